@@ -1,0 +1,282 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X Noise ChaChaPoly record engine (BASELINE.json).
+
+Metric: GiB/s of ChaChaPoly AEAD over device-resident 1 KiB Noise records.
+Workload (default, BASELINE config 2 = configs[1]): per GPU, R = 2^20 records
+of 1024 B under one post-handshake key k = 00..1f, nonces n = rank*R + i,
+plaintext from splitmix64(seed 0x4E4F495345).  One step = encrypt all R
+records (pt -> ct||tag) + decrypt all R records (ct||tag -> pt, tag verified),
+two kernel launches on one HIP stream.  `value` counts plaintext bytes through
+the AEAD (encrypt + decrypt) of all ranks / wall time of the K timed steps
+(max over ranks), in GiB/s (2^30 B/s).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
+                    [--no-cpu-baseline] [--host-inclusive]
+
+N > 1 is launched by torch.distributed.run, one process per GPU; records are
+sharded per GPU with no data-path collective (weak scaling: each rank owns
+its own R records and nonce range).  torch.distributed (RCCL) is used only
+for the barrier and the max-over-ranks of the elapsed time.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "noise-cpp_amd", "python"))
+
+import noise_amd  # noqa: E402
+
+SEED = 0x4E4F495345
+KEY = bytes(range(32))
+HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md)
+GIB = float(1 << 30)
+
+
+def log(msg):
+    print("[bench] " + msg, file=sys.stderr, flush=True)
+
+
+def shard(total, rank, world):
+    """Contiguous [lo, hi) slice of `total` units for `rank` (strong scaling)."""
+    return total * rank // world, total * (rank + 1) // world
+
+
+def pmc_traffic(workload):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any
+    (profiles/*/pmc_traffic.json, written from a separate --pmc pass)."""
+    best = None
+    pdir = os.path.join(ROOT, "profiles")
+    if os.path.isdir(pdir):
+        for sub in sorted(os.listdir(pdir)):
+            f = os.path.join(pdir, sub, "pmc_traffic.json")
+            if os.path.exists(f):
+                d = json.load(open(f))
+                if d.get("workload") == workload:
+                    best = d
+    return best
+
+
+def cpu_baseline(seconds=1.5, threads=None):
+    """Reference monocypher.c (oracle/_ref) -- or the build's C restatement
+    if _ref is absent -- on this host's cores: 1 KiB records, encrypt +
+    decrypt, repeated passes of 2^15 records until `seconds` of wall time."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    orc = oracle_lib.Oracle()
+    threads = threads or min(16, os.cpu_count() or 1)
+    L, R = 1024, 1 << 15
+    pt = np.frombuffer(orc.synthetic(R * L, SEED), dtype=np.uint8).copy()
+    ct = np.zeros(R * (L + 16), dtype=np.uint8)
+    back = np.zeros(R * L, dtype=np.uint8)
+    if orc.ref is not None:
+        kind = "reference"
+        fails = ctypes.c_int(0)
+
+        def run(dec):
+            if dec:
+                return orc.ref.ref_batch_uniform(1, KEY, 0, ct.ctypes.data, L + 16, back.ctypes.data,
+                                                 L, L, R, threads, ctypes.byref(fails))
+            return orc.ref.ref_batch_uniform(0, KEY, 0, pt.ctypes.data, L, ct.ctypes.data, L + 16,
+                                             L, R, threads, ctypes.byref(fails))
+    else:
+        kind = "port"
+
+        def run(dec):
+            if dec:
+                return orc.lib.oracle_batch_uniform(1, KEY, 0, ct.ctypes.data, L + 16,
+                                                    back.ctypes.data, L, L, R, threads, None)
+            return orc.lib.oracle_batch_uniform(0, KEY, 0, pt.ctypes.data, L, ct.ctypes.data,
+                                                L + 16, L, R, threads, None)
+    run(False)  # warm
+    t = 0.0
+    passes = 0
+    while t < seconds:
+        t += run(False) + run(True)
+        passes += 1
+    assert np.array_equal(pt, back), "cpu baseline round trip failed"
+    value = passes * 2 * R * L / t / GIB
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(value, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+            "sample": "%d passes x %d x 1 KiB records encrypt+decrypt (%.1f s wall, %d threads, "
+                      "%s, CPU %s)" % (passes, R, t, threads,
+                                       "monocypher.c via oracle/_ref" if kind == "reference"
+                                       else "oracle/chachapoly_oracle.c", model)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
+    ap.add_argument("--records", type=int, default=0, help="override records per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-inclusive", action="store_true",
+                    help="also time the pinned-host H2D->kernel->D2H pipeline (DESIGN.md)")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    noise_amd.load()
+    stream = torch.cuda.current_stream()
+
+    cfg = args.config
+    if cfg == 2:
+        R, L = args.records or (1 << 20), 1024
+        workload = "cfg2: 2^20 x 1 KiB records per GPU, one key, encrypt+decrypt round trip"
+        if args.records:
+            workload = "cfg2-shape: %d x 1 KiB records per GPU" % R
+        n_base = rank * R
+    elif cfg == 5:  # strong scaling: 8 Mi x 4 KiB split over the GPUs
+        total = args.records or (8 << 20)
+        lo, hi = shard(total, rank, world)
+        R, L = hi - lo, 4096
+        n_base = lo
+        workload = "cfg5: %d x 4 KiB records total, sharded over %d GPU(s)" % (total, world)
+    else:
+        raise SystemExit("configs 3/4 are parity-test shapes; bench line uses 2 (or 5)")
+    in_stride, ct_stride = L, L + 16
+
+    d_pt = torch.empty(R * L, dtype=torch.uint8, device="cuda")
+    noise_amd.fill_synthetic(d_pt, R * L, SEED, offset=n_base * L)
+    d_ct = torch.empty(R * ct_stride, dtype=torch.uint8, device="cuda")
+    d_back = torch.empty(R * L, dtype=torch.uint8, device="cuda")
+    d_st = torch.empty(R, dtype=torch.uint8, device="cuda")
+
+    def step(evs=None):
+        if evs:
+            evs[0].record(stream)
+        noise_amd.encrypt_uniform(KEY, n_base, d_pt, in_stride, d_ct, ct_stride, L, R, stream=stream)
+        if evs:
+            evs[1].record(stream)
+        noise_amd.decrypt_uniform(KEY, n_base, d_ct, ct_stride, d_back, in_stride, L, d_st, R,
+                                  stream=stream)
+        if evs:
+            evs[2].record(stream)
+
+    log("rank %d/%d: %d records x %d B, warmup %d" % (rank, world, R, L, args.warmup))
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # correctness of what is about to be timed: all tags verify, round trip exact
+    ok = int(d_st.sum().item()) == 0 and torch.equal(d_pt, d_back)
+    if not ok:
+        raise SystemExit("round trip failed on rank %d" % rank)
+
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        nrec_all = torch.tensor([R], dtype=torch.int64, device="cuda")
+        dist.all_reduce(nrec_all)
+        total_rec = int(nrec_all.item())
+    else:
+        total_rec = R
+    enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+    dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+    log("enc %.3f ms, dec %.3f ms per launch; step %.3f ms" %
+        (enc_ms, dec_ms, elapsed * 1e3 / args.steps))
+
+    total_bytes = 2.0 * total_rec * L * args.steps  # plaintext through AEAD (enc + dec)
+    value = total_bytes / elapsed / GIB
+
+    # roofline of the dominant kernel (algorithmic bytes per launch / its
+    # average duration from the HIP events on its own stream)
+    enc_bytes = R * (L + L + 16)        # read pt, write ct||tag
+    dec_bytes = R * (L + 16 + L + 1)    # read ct||tag, write pt + status byte
+    if enc_ms >= dec_ms:
+        kname, kbytes, kms = "k_aead_uniform<encrypt>", enc_bytes, enc_ms
+    else:
+        kname, kbytes, kms = "k_aead_uniform<decrypt>", dec_bytes, dec_ms
+    achieved = kbytes / (kms * 1e-3)
+    pmc = pmc_traffic(workload)
+    traffic = None
+    if pmc and kname in pmc.get("per_launch_bytes", {}):
+        traffic = pmc["per_launch_bytes"][kname]
+    roof = {"bound": "hbm", "kernel": kname, "achieved": round(achieved / 1e9, 1),
+            "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
+            "traffic": traffic, "algorithmic_bytes_per_launch": kbytes,
+            "avg_launch_ms": round(kms, 4),
+            "enc_ms": round(enc_ms, 4), "dec_ms": round(dec_ms, 4)}
+
+    line = {"metric": "GiB/s ChaChaPoly AEAD over device-resident 1 KiB Noise records, 1 & 8 GPU"
+                      if L == 1024 else "GiB/s ChaChaPoly AEAD over device-resident 4 KiB records",
+            "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+            "higher_is_better": True, "scaling": "weak" if cfg == 2 else "strong",
+            "vs_baseline": None, "dtype": "u32", "data": "synthetic (splitmix64)",
+            "config": {"workload": workload, "records_per_gpu": R, "record_bytes": L,
+                       "ct_stride": ct_stride, "keys": 1, "bytes_counted":
+                       "plaintext bytes through the AEAD, encrypt + decrypt",
+                       "parallelism": "records sharded per GPU, no collective"},
+            "roofline": roof}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("cpu baseline ...")
+        line["cpu_baseline"] = cpu_baseline()
+    if rank == 0 and args.host_inclusive:
+        line["host_inclusive"] = host_inclusive(R, L)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def host_inclusive(R, L):
+    """Pinned host buffers -> chunked H2D || kernel || D2H pipeline (3 streams)."""
+    import torch
+    lib = noise_amd.load()
+    pt = torch.empty(R * L, dtype=torch.uint8).pin_memory()
+    d = torch.empty(R * L, dtype=torch.uint8, device="cuda")
+    noise_amd.fill_synthetic(d, R * L, SEED)
+    pt.copy_(d)
+    del d
+    ct = torch.empty(R * (L + 16), dtype=torch.uint8).pin_memory()
+    back = torch.empty(R * L, dtype=torch.uint8).pin_memory()
+    st = torch.empty(R, dtype=torch.uint8).pin_memory()
+    te, td = ctypes.c_double(), ctypes.c_double()
+    for _ in range(2):
+        assert lib.noise_gpu_encrypt_uniform_host(KEY, 0, ctypes.c_void_p(pt.data_ptr()), L,
+                                                  ctypes.c_void_p(ct.data_ptr()), L + 16, L, R,
+                                                  ctypes.byref(te)) == 0
+        assert lib.noise_gpu_decrypt_uniform_host(KEY, 0, ctypes.c_void_p(ct.data_ptr()), L + 16,
+                                                  ctypes.c_void_p(back.data_ptr()), L, L,
+                                                  ctypes.c_void_p(st.data_ptr()), R,
+                                                  ctypes.byref(td)) == 0
+    assert torch.equal(pt, back) and int(st.sum()) == 0
+    return {"encrypt_GiBps": round(R * L / te.value / GIB, 2),
+            "decrypt_GiBps": round(R * L / td.value / GIB, 2),
+            "note": "pinned host -> device -> host, 32 MiB chunks over 3 HIP streams"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,182 @@
+/*
+ * noise_gpu.h -- C ABI of the MI355X (gfx950) Noise transport-record AEAD
+ * engine (ChaChaPoly, Noise nonce framing).
+ *
+ * This is the drop-in boundary under noise::CipherState.  In the reference
+ * (ethindp/noise-cpp @ 2025-09-05) every transport record goes
+ *     CipherState::encrypt_with_ad / decrypt_with_ad   noise.cpp:393-427
+ *  -> noise::encrypt / noise::decrypt                   noise.cpp:202-281
+ *  -> crypto_aead_init_ietf + crypto_aead_write/_read    monocypher.c:2891-2929
+ * and CipherState::rekey (noise.cpp:429-439) calls noise::encrypt at nonce
+ * 2^64-2.  The functions below replace that chain: the C++20 CipherState in
+ * noise-cpp_amd/host/ (same class surface as noise.h:99-115) calls them,
+ * and device-resident batch callers may call them directly.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  `d_` pointers are device (HBM)
+ *    pointers, `h_` pointers host pointers.  `stream` is a hipStream_t
+ *    passed as void* (NULL = the legacy default stream).
+ *  - Device-pointer functions are asynchronous on `stream`: argument
+ *    checks happen at the call, results are ready when the stream is.
+ *  - No function throws; every function returns a noise_gpu_status.
+ *  - Record i of a uniform batch uses nonce (nonce0 + i) mod 2^64, the
+ *    Noise 12-byte nonce 0^32 || LE64(n) (noise.cpp:207-215).
+ *  - Ciphertext records are the Noise wire format ct || tag: len+16 bytes.
+ *  - Nonce-limit (noise.cpp:398-400, 416-418: n == 2^64-2 is refused) is a
+ *    host-object rule; the batch functions below encrypt whatever nonces
+ *    they are given.  The CipherState shim applies the rule per record.
+ */
+#ifndef NOISE_GPU_H
+#define NOISE_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum noise_gpu_status {
+  NOISE_GPU_OK = 0,
+  NOISE_GPU_E_NONCE = 1, /* nonce limit; reference std::out_of_range      */
+  NOISE_GPU_E_MAC = 2,   /* tag mismatch; reference std::invalid_argument */
+  NOISE_GPU_E_ARG = 3,   /* bad argument (null, size, alignment, range)   */
+  NOISE_GPU_E_HIP = 4,   /* HIP runtime error (see noise_gpu_last_error)  */
+  NOISE_GPU_E_NODEV = 5  /* no gfx950 device visible                      */
+} noise_gpu_status;
+
+/* Per-record descriptor for many-session / variable-length batches.
+ * Offsets are byte offsets into the d_in / d_out / d_ad buffers. */
+typedef struct noise_gpu_record {
+  uint64_t in_off;  /* plaintext (encrypt) or ct||tag (decrypt) */
+  uint64_t out_off; /* ct||tag (encrypt) or plaintext (decrypt)  */
+  uint64_t nonce;   /* Noise n for this record                   */
+  uint64_t ad_off;  /* associated data offset (ignored if ad_len == 0) */
+  uint32_t len;     /* plaintext length, <= 65519 for Noise messages */
+  uint32_t ad_len;  /* associated data length                    */
+  uint32_t key_idx; /* row of the [nkeys][32] key table          */
+  uint32_t reserved;
+} noise_gpu_record;
+
+/* Per-record status codes written by the decrypt functions. */
+#define NOISE_GPU_REC_OK 0u
+#define NOISE_GPU_REC_BAD_MAC 1u
+
+/* ---- runtime ---------------------------------------------------------- */
+
+/* Version string of the engine ("noise-mi355x <ver> gfx950"). */
+const char *noise_gpu_version(void);
+/* Human-readable text of a status code. */
+const char *noise_gpu_strerror(int status);
+/* Text of the last HIP error seen by this thread (empty if none). */
+const char *noise_gpu_last_error(void);
+/* Number of visible HIP devices (0 without a GPU). */
+int noise_gpu_device_count(int *count);
+
+/* ---- device-resident uniform batches (the BASELINE hot path) -----------
+ * nrec records of exactly `len` plaintext bytes under one 32-byte key.
+ * Record i: input at d_in + i*in_stride, output at d_out + i*out_stride,
+ * associated data at d_ad + i*ad_stride (ad_stride 0 = the same AD for every
+ * record; ad_len 0 = no AD, the transport case).
+ * Encrypt writes len+16 bytes per record (ct || tag).  in == out with equal
+ * strides is in-place; other overlaps are undefined.
+ * Decrypt reads len+16 bytes per record, writes len plaintext bytes only
+ * where the tag verifies, and writes d_status[i] (NOISE_GPU_REC_*).  A
+ * record whose tag fails is left as it was when in-place (the reference
+ * leaves the buffer untouched, monocypher.c:2919-2926) and is zeroed in an
+ * out-of-place output (no unauthenticated plaintext is left behind).
+ * Records are processed one per lane; 16-byte aligned pointers/strides and
+ * len % 16 == 0 take the vector path, anything else a byte-granular path. */
+int noise_gpu_encrypt_uniform(const uint8_t h_key[32], uint64_t nonce0,
+                              const uint8_t *d_in, uint64_t in_stride,
+                              uint8_t *d_out, uint64_t out_stride,
+                              uint32_t len, const uint8_t *d_ad,
+                              uint64_t ad_stride, uint32_t ad_len,
+                              uint64_t nrec, void *stream);
+
+int noise_gpu_decrypt_uniform(const uint8_t h_key[32], uint64_t nonce0,
+                              const uint8_t *d_in, uint64_t in_stride,
+                              uint8_t *d_out, uint64_t out_stride,
+                              uint32_t len, const uint8_t *d_ad,
+                              uint64_t ad_stride, uint32_t ad_len,
+                              uint8_t *d_status, uint64_t nrec, void *stream);
+
+/* ---- device-resident descriptor batches (many sessions, mixed sizes) ---
+ * d_keys: [nkeys][32] key table in HBM; d_recs: nrec descriptors in HBM.
+ * Same in-place / failure rules as the uniform functions. */
+int noise_gpu_encrypt_records(const uint8_t *d_keys, uint32_t nkeys,
+                              const noise_gpu_record *d_recs, uint64_t nrec,
+                              const uint8_t *d_in, uint8_t *d_out,
+                              const uint8_t *d_ad, void *stream);
+
+int noise_gpu_decrypt_records(const uint8_t *d_keys, uint32_t nkeys,
+                              const noise_gpu_record *d_recs, uint64_t nrec,
+                              const uint8_t *d_in, uint8_t *d_out,
+                              const uint8_t *d_ad, uint8_t *d_status,
+                              void *stream);
+
+/* REKEY of every key in a device key table, in place:
+ * k <- ENCRYPT(k, 2^64-2, empty, 0^32)[0..32)   (noise.cpp:429-439). */
+int noise_gpu_rekey_keys(uint8_t *d_keys, uint64_t nkeys, void *stream);
+
+/* ---- host-buffer entry points (synchronous) ----------------------------
+ * Used by the CipherState shim for single records (encrypt_with_ad /
+ * decrypt_with_ad / rekey).  They stage through pinned host memory and a
+ * per-thread device scratch area, run the same kernels and synchronise.
+ * h_buf holds len plaintext bytes and has room for len+16 (encrypt), or
+ * holds ct_len = len+16 bytes (decrypt, plaintext written to h_buf[0..len)
+ * on success, h_buf untouched and NOISE_GPU_E_MAC returned on failure). */
+int noise_gpu_encrypt_host(const uint8_t h_key[32], uint64_t nonce,
+                           const uint8_t *h_ad, size_t ad_len, uint8_t *h_buf,
+                           size_t len);
+int noise_gpu_decrypt_host(const uint8_t h_key[32], uint64_t nonce,
+                           const uint8_t *h_ad, size_t ad_len, uint8_t *h_buf,
+                           size_t ct_len);
+int noise_gpu_rekey_host(uint8_t h_key[32]);
+
+/* Descriptor batch between HOST buffers (synchronous): the key table
+ * (nkeys x 32 B), descriptors, h_in[0..in_bytes) and h_ad[0..ad_bytes) are
+ * staged to the device, the records kernel runs, h_out[0..out_bytes) (and
+ * h_status[nrec] for decrypt) are copied back.  Used by
+ * CipherState::encrypt_batch / decrypt_batch. */
+int noise_gpu_encrypt_records_host(const uint8_t *h_keys, uint32_t nkeys,
+                                   const noise_gpu_record *h_recs,
+                                   uint64_t nrec, const uint8_t *h_in,
+                                   uint64_t in_bytes, uint8_t *h_out,
+                                   uint64_t out_bytes, const uint8_t *h_ad,
+                                   uint64_t ad_bytes);
+int noise_gpu_decrypt_records_host(const uint8_t *h_keys, uint32_t nkeys,
+                                   const noise_gpu_record *h_recs,
+                                   uint64_t nrec, const uint8_t *h_in,
+                                   uint64_t in_bytes, uint8_t *h_out,
+                                   uint64_t out_bytes, const uint8_t *h_ad,
+                                   uint64_t ad_bytes, uint8_t *h_status);
+
+/* Uniform batch between HOST buffers: pinned-staged, chunked and
+ * double-buffered (H2D copy || kernel || D2H copy on separate streams).
+ * Encrypt: h_in records of len bytes (stride in_stride) -> h_out records of
+ * len+16 (stride out_stride).  Decrypt: the reverse, with h_status[nrec].
+ * *seconds receives the wall time of the whole transfer-inclusive run. */
+int noise_gpu_encrypt_uniform_host(const uint8_t h_key[32], uint64_t nonce0,
+                                   const uint8_t *h_in, uint64_t in_stride,
+                                   uint8_t *h_out, uint64_t out_stride,
+                                   uint32_t len, uint64_t nrec,
+                                   double *seconds);
+int noise_gpu_decrypt_uniform_host(const uint8_t h_key[32], uint64_t nonce0,
+                                   const uint8_t *h_in, uint64_t in_stride,
+                                   uint8_t *h_out, uint64_t out_stride,
+                                   uint32_t len, uint8_t *h_status,
+                                   uint64_t nrec, double *seconds);
+
+/* ---- synthetic data (bench / tests) ------------------------------------
+ * Fill d_dst[0..nbytes) with the splitmix64 stream: byte j = byte (j & 7)
+ * of mix64(seed + ((offset+j)/8 + 1) * 0x9e3779b97f4a7c15), offset-relative
+ * so shards of one logical buffer can be generated independently. */
+int noise_gpu_fill_synthetic(uint8_t *d_dst, uint64_t offset, uint64_t nbytes,
+                             uint64_t seed, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NOISE_GPU_H */

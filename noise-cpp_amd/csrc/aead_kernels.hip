@@ -1,0 +1,182 @@
+// aead_kernels.hip -- gfx950 kernels of the Noise ChaChaPoly record engine
+// and their host-side launchers (called by noise_gpu_api.hip).
+//
+//   k_encrypt_uniform / k_decrypt_uniform   one key, fixed length, implicit
+//                                            nonce0 + i, fixed strides (the
+//                                            BASELINE config-2 hot path)
+//   k_encrypt_records / k_decrypt_records   descriptor batches: per-record
+//                                            key row, nonce, length, offsets
+//   k_rekey                                  CipherState::rekey on a table
+//   k_fill_synthetic                         splitmix64 test/bench data
+//
+// One lane = one record (chachapoly_device.hpp).  Launch: 256-thread
+// workgroups, one record per thread; the grid covers nrec.
+#include "chachapoly_device.hpp"
+#include "launchers.hpp"
+
+namespace noise_amd {
+
+constexpr int kBlock = 256;
+
+struct KeyArg {
+  uint32_t w[8];
+};
+
+template <bool DECRYPT, bool VEC>
+__global__ __launch_bounds__(kBlock) void k_aead_uniform(
+    KeyArg key, uint64_t nonce0, const uint8_t *__restrict__ in,
+    uint64_t in_stride, uint8_t *out, uint64_t out_stride, uint32_t len,
+    const uint8_t *ad, uint64_t ad_stride, uint32_t ad_len, uint8_t *status,
+    uint64_t nrec) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= nrec) return;
+  uint32_t k[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) k[j] = key.w[j];
+  const bool ok = aead_record<DECRYPT, VEC>(
+      k, nonce0 + i, in + i * in_stride, out + i * out_stride, len,
+      ad + i * ad_stride, ad_len);
+  if (DECRYPT) status[i] = ok ? 0u : 1u;
+}
+
+template <bool DECRYPT>
+__global__ __launch_bounds__(kBlock) void k_aead_records(
+    const uint8_t *__restrict__ keys, uint32_t nkeys,
+    const noise_gpu_record *__restrict__ recs, uint64_t nrec,
+    const uint8_t *in, uint8_t *out, const uint8_t *ad, uint8_t *status) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= nrec) return;
+  const noise_gpu_record r = recs[i];
+  if (r.key_idx >= nkeys) {  // host validated; never index out of the table
+    if (DECRYPT) status[i] = 1u;
+    return;
+  }
+  const uint4 *kp = reinterpret_cast<const uint4 *>(keys + 32u * r.key_idx);
+  const uint4 ka = kp[0], kb = kp[1];
+  const uint32_t k[8] = {ka.x, ka.y, ka.z, ka.w, kb.x, kb.y, kb.z, kb.w};
+  const uint8_t *src = in + r.in_off;
+  uint8_t *dst = out + r.out_off;
+  const bool vec = ((reinterpret_cast<uintptr_t>(src) |
+                     reinterpret_cast<uintptr_t>(dst) | r.len) & 15u) == 0;
+  bool ok;
+  if (vec)
+    ok = aead_record<DECRYPT, true>(k, r.nonce, src, dst, r.len, ad + r.ad_off, r.ad_len);
+  else
+    ok = aead_record<DECRYPT, false>(k, r.nonce, src, dst, r.len, ad + r.ad_off, r.ad_len);
+  if (DECRYPT) status[i] = ok ? 0u : 1u;
+}
+
+// REKEY: k <- ENCRYPT(k, 2^64-2, empty, 0^32)[0..32) = first 32 keystream
+// bytes of block 1 at nonce 2^64-2 (the zero plaintext makes ct = ks).
+__global__ __launch_bounds__(kBlock) void k_rekey(uint8_t *keys, uint64_t nkeys) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= nkeys) return;
+  uint4 *kp = reinterpret_cast<uint4 *>(keys + 32u * i);
+  const uint4 ka = kp[0], kb = kp[1];
+  const uint32_t k[8] = {ka.x, ka.y, ka.z, ka.w, kb.x, kb.y, kb.z, kb.w};
+  const uint64_t n = ~0ull - 1ull;
+  uint32_t ks[16];
+  chacha20_block(k, 1u, (uint32_t)n, (uint32_t)(n >> 32), ks);
+  kp[0] = make_uint4(ks[0], ks[1], ks[2], ks[3]);
+  kp[1] = make_uint4(ks[4], ks[5], ks[6], ks[7]);
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+// 16 bytes per thread; `offset` and d_dst 16-byte aligned on this path.
+__global__ __launch_bounds__(kBlock) void k_fill_synthetic_vec(
+    uint4 *dst, uint64_t offset, uint64_t nvec, uint64_t seed) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= nvec) return;
+  const uint64_t w = (offset >> 3) + 2 * i;
+  const uint64_t a = mix64(seed + (w + 1) * 0x9e3779b97f4a7c15ull);
+  const uint64_t b = mix64(seed + (w + 2) * 0x9e3779b97f4a7c15ull);
+  dst[i] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b,
+                      (uint32_t)(b >> 32));
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill_synthetic_bytes(
+    uint8_t *dst, uint64_t offset, uint64_t nbytes, uint64_t seed) {
+  const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= nbytes) return;
+  const uint64_t b = offset + j;
+  dst[j] = (uint8_t)(mix64(seed + ((b >> 3) + 1) * 0x9e3779b97f4a7c15ull) >>
+                     (8 * (b & 7)));
+}
+
+static inline dim3 grid_for(uint64_t n) {
+  return dim3((unsigned)((n + kBlock - 1) / kBlock));
+}
+
+hipError_t launch_aead_uniform(bool decrypt, const uint32_t key[8],
+                               uint64_t nonce0, const uint8_t *in,
+                               uint64_t in_stride, uint8_t *out,
+                               uint64_t out_stride, uint32_t len,
+                               const uint8_t *ad, uint64_t ad_stride,
+                               uint32_t ad_len, uint8_t *status, uint64_t nrec,
+                               hipStream_t stream) {
+  if (nrec == 0) return hipSuccess;
+  KeyArg k;
+  for (int j = 0; j < 8; ++j) k.w[j] = key[j];
+  const bool vec = ((reinterpret_cast<uintptr_t>(in) |
+                     reinterpret_cast<uintptr_t>(out) | in_stride |
+                     out_stride | len) & 15u) == 0;
+  const dim3 g = grid_for(nrec), b(kBlock);
+  if (decrypt) {
+    if (vec)
+      hipLaunchKernelGGL((k_aead_uniform<true, true>), g, b, 0, stream, k, nonce0, in, in_stride, out, out_stride, len, ad, ad_stride, ad_len, status, nrec);
+    else
+      hipLaunchKernelGGL((k_aead_uniform<true, false>), g, b, 0, stream, k, nonce0, in, in_stride, out, out_stride, len, ad, ad_stride, ad_len, status, nrec);
+  } else {
+    if (vec)
+      hipLaunchKernelGGL((k_aead_uniform<false, true>), g, b, 0, stream, k, nonce0, in, in_stride, out, out_stride, len, ad, ad_stride, ad_len, status, nrec);
+    else
+      hipLaunchKernelGGL((k_aead_uniform<false, false>), g, b, 0, stream, k, nonce0, in, in_stride, out, out_stride, len, ad, ad_stride, ad_len, status, nrec);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
+                               uint32_t nkeys, const noise_gpu_record *recs,
+                               uint64_t nrec, const uint8_t *in, uint8_t *out,
+                               const uint8_t *ad, uint8_t *status,
+                               hipStream_t stream) {
+  if (nrec == 0) return hipSuccess;
+  const dim3 g = grid_for(nrec), b(kBlock);
+  if (decrypt)
+    hipLaunchKernelGGL((k_aead_records<true>), g, b, 0, stream, keys, nkeys, recs, nrec, in, out, ad, status);
+  else
+    hipLaunchKernelGGL((k_aead_records<false>), g, b, 0, stream, keys, nkeys, recs, nrec, in, out, ad, status);
+  return hipGetLastError();
+}
+
+hipError_t launch_rekey(uint8_t *keys, uint64_t nkeys, hipStream_t stream) {
+  if (nkeys == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rekey, grid_for(nkeys), dim3(kBlock), 0, stream, keys, nkeys);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_synthetic(uint8_t *dst, uint64_t offset,
+                                 uint64_t nbytes, uint64_t seed,
+                                 hipStream_t stream) {
+  if (nbytes == 0) return hipSuccess;
+  const bool vec = ((reinterpret_cast<uintptr_t>(dst) | offset) & 15u) == 0;
+  uint64_t head = 0;
+  if (vec) {
+    const uint64_t nvec = nbytes >> 4;
+    if (nvec)
+      hipLaunchKernelGGL(k_fill_synthetic_vec, grid_for(nvec), dim3(kBlock), 0, stream,
+                         reinterpret_cast<uint4 *>(dst), offset, nvec, seed);
+    head = nvec << 4;
+  }
+  if (head < nbytes)
+    hipLaunchKernelGGL(k_fill_synthetic_bytes, grid_for(nbytes - head), dim3(kBlock), 0,
+                       stream, dst + head, offset + head, nbytes - head, seed);
+  return hipGetLastError();
+}
+
+}  // namespace noise_amd

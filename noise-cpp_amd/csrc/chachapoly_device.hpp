@@ -1,0 +1,310 @@
+// chachapoly_device.hpp -- gfx950 device arithmetic for the Noise ChaChaPoly
+// record engine: ChaCha20 block function, Poly1305 block/finalise, and the
+// per-record AEAD walk (Noise nonce framing, ct || tag layout).
+//
+// Mapping (DESIGN.md "Kernels"): ONE LANE = ONE RECORD.  A lane derives its
+// record's one-time Poly1305 key from ChaCha block 0, then walks the record
+// in 64-byte chunks: ChaCha block (1 + chunk) -> XOR -> 4 Poly1305 blocks.
+// Everything stays in VGPRs; nothing is shared between lanes, so there is
+// no LDS, no barrier and no cross-lane reduction.  This is the op-minimal
+// mapping: 1 KiB costs exactly 17 ChaCha blocks + 65 Poly1305 blocks per
+// record, with no r-power precomputation (a k-lane split of one record's
+// Poly1305 would need r^2..r^k per record, +30-120 % Poly work).
+//
+// Arithmetic references (what is computed, not how):
+//   ChaCha20 quarter-round / 20 rounds   monocypher.c:169-200
+//   keystream feed-forward, counter      monocypher.c:219-253
+//   Poly1305 clamp / block / final       monocypher.c:366-440
+//   AEAD layout ad|pad|ct|pad|lens       monocypher.c:2858-2873
+//   Noise nonce 0^32 || LE64(n)          noise.cpp:207-215
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace noise_amd {
+
+// "expand 32-byte k"
+constexpr uint32_t kSigma0 = 0x61707865u, kSigma1 = 0x3320646eu,
+                   kSigma2 = 0x79622d32u, kSigma3 = 0x6b206574u;
+
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int n) {
+  // one v_alignbit_b32
+  return __builtin_amdgcn_alignbit(x, x, 32 - n);
+}
+
+#define NOISE_QR(a, b, c, d)              \
+  a += b; d = rotl32(d ^ a, 16);          \
+  c += d; b = rotl32(b ^ c, 12);          \
+  a += b; d = rotl32(d ^ a, 8);           \
+  c += d; b = rotl32(b ^ c, 7);
+
+// ChaCha20 block with IETF word layout: x12 = block counter, x13 = 0 (the
+// four zero bytes of the Noise nonce), x14/x15 = lo/hi 32 bits of n.
+// ks[] receives the 16 keystream words (after the feed-forward add).
+// When k[] and ctr are wave-uniform (single-key batches) the compiler keeps
+// them in SGPRs and the first-round columns 0/1 run on the scalar unit.
+__device__ __forceinline__ void chacha20_block(const uint32_t k[8],
+                                               uint32_t ctr, uint32_t n_lo,
+                                               uint32_t n_hi, uint32_t ks[16]) {
+  uint32_t x0 = kSigma0, x1 = kSigma1, x2 = kSigma2, x3 = kSigma3;
+  uint32_t x4 = k[0], x5 = k[1], x6 = k[2], x7 = k[3];
+  uint32_t x8 = k[4], x9 = k[5], x10 = k[6], x11 = k[7];
+  uint32_t x12 = ctr, x13 = 0, x14 = n_lo, x15 = n_hi;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    NOISE_QR(x0, x4, x8, x12)
+    NOISE_QR(x1, x5, x9, x13)
+    NOISE_QR(x2, x6, x10, x14)
+    NOISE_QR(x3, x7, x11, x15)
+    NOISE_QR(x0, x5, x10, x15)
+    NOISE_QR(x1, x6, x11, x12)
+    NOISE_QR(x2, x7, x8, x13)
+    NOISE_QR(x3, x4, x9, x14)
+  }
+  ks[0] = x0 + kSigma0;  ks[1] = x1 + kSigma1;
+  ks[2] = x2 + kSigma2;  ks[3] = x3 + kSigma3;
+  ks[4] = x4 + k[0];     ks[5] = x5 + k[1];
+  ks[6] = x6 + k[2];     ks[7] = x7 + k[3];
+  ks[8] = x8 + k[4];     ks[9] = x9 + k[5];
+  ks[10] = x10 + k[6];   ks[11] = x11 + k[7];
+  ks[12] = x12 + ctr;    ks[13] = x13;
+  ks[14] = x14 + n_lo;   ks[15] = x15 + n_hi;
+}
+
+// Poly1305 in radix 2^32 (four 32-bit limbs + a small 2^128 limb), which
+// turns each block into 20 v_mad_u64_u32 + ~15 add/carry ops.  The clamp
+// makes r1..r3 multiples of 4, so 2^128 * r_j == 5 * (r_j / 4) (mod p)
+// folds the high partial products back with rr_j = r_j + (r_j >> 2).
+struct Poly1305 {
+  uint32_t h0, h1, h2, h3, h4;
+  uint32_t r0, r1, r2, r3;
+  uint32_t rr0, rr1, rr2, rr3;  // rr0 = 5*(r0>>2); rr_j = 5*(r_j/4)
+  uint32_t r0lo;                // r0 & 3
+  uint32_t s0, s1, s2, s3;      // the "s" half of the one-time key
+};
+
+// one-time key = keystream block 0 words 0..7 (monocypher.c:2903, 366-375)
+__device__ __forceinline__ void poly_init(Poly1305 &p, const uint32_t otk[16]) {
+  p.r0 = otk[0] & 0x0fffffffu;
+  p.r1 = otk[1] & 0x0ffffffcu;
+  p.r2 = otk[2] & 0x0ffffffcu;
+  p.r3 = otk[3] & 0x0ffffffcu;
+  p.rr0 = (p.r0 >> 2) * 5u;
+  p.rr1 = p.r1 + (p.r1 >> 2);
+  p.rr2 = p.r2 + (p.r2 >> 2);
+  p.rr3 = p.r3 + (p.r3 >> 2);
+  p.r0lo = p.r0 & 3u;
+  p.s0 = otk[4]; p.s1 = otk[5]; p.s2 = otk[6]; p.s3 = otk[7];
+  p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0;
+}
+
+__device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
+  return (uint64_t)a * b + c;  // v_mad_u64_u32
+}
+
+// h <- (h + m + 2^128) * r  (partially reduced: h4 <= 4 on exit).
+// Written with explicit 32-bit carry chains (v_add_co / v_addc_co) so the
+// compiler never widens limbs to 64 bits: 5 + 20 mad64 + ~10 ops per block.
+__device__ __forceinline__ void poly_block(Poly1305 &p, uint32_t m0,
+                                           uint32_t m1, uint32_t m2,
+                                           uint32_t m3) {
+  unsigned c;
+  // s = h + m + 2^128 with full carry propagation (s4 <= 6)
+  const uint32_t s0 = __builtin_addc(p.h0, m0, 0u, &c);
+  const uint32_t s1 = __builtin_addc(p.h1, m1, c, &c);
+  const uint32_t s2 = __builtin_addc(p.h2, m2, c, &c);
+  const uint32_t s3 = __builtin_addc(p.h3, m3, c, &c);
+  const uint32_t s4 = p.h4 + c + 1u;
+  // column sums, each < 2^63
+  const uint64_t x0 = mad64(s0, p.r0, mad64(s1, p.rr3, mad64(s2, p.rr2, mad64(s3, p.rr1, mad64(s4, p.rr0, 0)))));
+  const uint64_t x1 = mad64(s0, p.r1, mad64(s1, p.r0, mad64(s2, p.rr3, mad64(s3, p.rr2, mad64(s4, p.rr1, 0)))));
+  const uint64_t x2 = mad64(s0, p.r2, mad64(s1, p.r1, mad64(s2, p.r0, mad64(s3, p.rr3, mad64(s4, p.rr2, 0)))));
+  const uint64_t x3 = mad64(s0, p.r3, mad64(s1, p.r2, mad64(s2, p.r1, mad64(s3, p.r0, mad64(s4, p.rr3, 0)))));
+  const uint32_t x4 = __umul24(s4, p.r0lo);  // tiny * tiny
+  // partial reduction: fold everything at and above 2^130 back as *5
+  const uint32_t u5 = x4 + (uint32_t)(x3 >> 32);
+  const uint32_t q = u5 >> 2;
+  p.h0 = __builtin_addc(q + (q << 2), (uint32_t)x0, 0u, &c);
+  p.h1 = __builtin_addc((uint32_t)x1, (uint32_t)(x0 >> 32), c, &c);
+  p.h2 = __builtin_addc((uint32_t)x2, (uint32_t)(x1 >> 32), c, &c);
+  p.h3 = __builtin_addc((uint32_t)x3, (uint32_t)(x2 >> 32), c, &c);
+  p.h4 = (u5 & 3u) + c;
+}
+
+// tag = (h mod 2^130-5) + s  mod 2^128  (monocypher.c:424-436)
+__device__ __forceinline__ void poly_final(const Poly1305 &p, uint32_t tag[4]) {
+  // carry of h + 5 into bit 130 says whether h >= p
+  uint64_t c = 5;
+  c = (c + p.h0) >> 32;
+  c = (c + p.h1) >> 32;
+  c = (c + p.h2) >> 32;
+  c = (c + p.h3) >> 32;
+  c += p.h4;
+  c = (c >> 2) * 5;  // 0 or 5
+  c += (uint64_t)p.h0 + p.s0;
+  tag[0] = (uint32_t)c;
+  c = (c >> 32) + (uint64_t)p.h1 + p.s1;
+  tag[1] = (uint32_t)c;
+  c = (c >> 32) + (uint64_t)p.h2 + p.s2;
+  tag[2] = (uint32_t)c;
+  c = (c >> 32) + (uint64_t)p.h3 + p.s3;
+  tag[3] = (uint32_t)c;
+}
+
+// ---------------------------------------------------------------- memory
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Byte-granular little-endian word load/store for unaligned records.
+__device__ __forceinline__ uint32_t ld_bytes(const uint8_t *p, int n) {
+  uint32_t w = 0;
+  for (int i = 0; i < n; ++i) w |= (uint32_t)p[i] << (8 * i);
+  return w;
+}
+__device__ __forceinline__ void st_bytes(uint8_t *p, uint32_t w, int n) {
+  for (int i = 0; i < n; ++i) p[i] = (uint8_t)(w >> (8 * i));
+}
+
+// Load `n` (0..16) bytes as 4 LE words, zero padded.  VEC: the 16 bytes
+// are 16-byte aligned and readable (n == 16 whenever VEC is used).
+template <bool VEC>
+__device__ __forceinline__ uint4 load16(const uint8_t *p, int n) {
+  if (VEC) {
+    // one global_load_dwordx4; records are streamed once (nontemporal)
+    const u32x4 w = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+    return make_uint4(w.x, w.y, w.z, w.w);
+  }
+  uint4 v;
+  v.x = ld_bytes(p, n >= 4 ? 4 : n);
+  v.y = n > 4 ? ld_bytes(p + 4, n >= 8 ? 4 : n - 4) : 0u;
+  v.z = n > 8 ? ld_bytes(p + 8, n >= 12 ? 4 : n - 8) : 0u;
+  v.w = n > 12 ? ld_bytes(p + 12, n - 12) : 0u;
+  return v;
+}
+template <bool VEC>
+__device__ __forceinline__ void store16(uint8_t *p, uint4 v, int n) {
+  if (VEC) {
+    // one aligned global_store_dwordx4 (a plain uint4 store may be
+    // re-split by the store merger into misaligned dwordx3/x4 pieces)
+    const u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4 *>(p));
+    return;
+  }
+  st_bytes(p, v.x, n >= 4 ? 4 : n);
+  if (n > 4) st_bytes(p + 4, v.y, n >= 8 ? 4 : n - 4);
+  if (n > 8) st_bytes(p + 8, v.z, n >= 12 ? 4 : n - 8);
+  if (n > 12) st_bytes(p + 12, v.w, n - 12);
+}
+
+// Poly1305 over `n` bytes of associated data, zero padded to 16.
+__device__ __forceinline__ void poly_ad(Poly1305 &p, const uint8_t *ad,
+                                        uint32_t n) {
+  for (uint32_t off = 0; off < n; off += 16) {
+    const int m = (n - off) >= 16 ? 16 : (int)(n - off);
+    const uint4 v = load16<false>(ad + off, m);
+    poly_block(p, v.x, v.y, v.z, v.w);
+  }
+}
+
+// --------------------------------------------------------- record walk
+// One AEAD record (Noise ENCRYPT / DECRYPT, noise.cpp:202-281 semantics).
+//   DECRYPT=false: in = plaintext[len]  -> out = ct[len] || tag[16]
+//   DECRYPT=true : in = ct[len]||tag    -> out = plaintext[len] if the tag
+//                  verifies; returns false on mismatch, and then restores
+//                  (in-place) or zeroes (out-of-place) the output.
+// VEC: in/out are 16-byte aligned and len % 16 == 0 (dwordx4 path).
+template <bool DECRYPT, bool VEC>
+__device__ __forceinline__ bool aead_record(const uint32_t k[8], uint64_t n,
+                                            const uint8_t *in, uint8_t *out,
+                                            uint32_t len, const uint8_t *ad,
+                                            uint32_t ad_len) {
+  const uint32_t n_lo = (uint32_t)n, n_hi = (uint32_t)(n >> 32);
+  Poly1305 p;
+  {
+    uint32_t otk[16];
+    chacha20_block(k, 0u, n_lo, n_hi, otk);
+    poly_init(p, otk);
+  }
+  if (ad_len) poly_ad(p, ad, ad_len);
+
+  const uint32_t nfull = len >> 6;
+  for (uint32_t c = 0; c < nfull; ++c) {
+    uint32_t ks[16];
+    chacha20_block(k, 1u + c, n_lo, n_hi, ks);
+    const uint8_t *src = in + 64u * c;
+    uint8_t *dst = out + 64u * c;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint4 v = load16<VEC>(src + 16 * q, 16);
+      uint4 o;
+      o.x = v.x ^ ks[4 * q + 0];
+      o.y = v.y ^ ks[4 * q + 1];
+      o.z = v.z ^ ks[4 * q + 2];
+      o.w = v.w ^ ks[4 * q + 3];
+      if (DECRYPT) poly_block(p, v.x, v.y, v.z, v.w);
+      else poly_block(p, o.x, o.y, o.z, o.w);
+      store16<VEC>(dst + 16 * q, o, 16);
+    }
+  }
+  const uint32_t rem = len & 63u;
+  if (rem) {
+    uint32_t ks[16];
+    chacha20_block(k, 1u + nfull, n_lo, n_hi, ks);
+    const uint8_t *src = in + 64u * nfull;
+    uint8_t *dst = out + 64u * nfull;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int m = (int)rem - 16 * q;
+      if (m <= 0) break;
+      const int nb = m >= 16 ? 16 : m;
+      const uint4 v = load16<VEC>(src + 16 * q, nb);
+      // keystream bytes past the record end must not reach the MAC: mask
+      const uint32_t m0 = nb >= 4 ? ~0u : (nb > 0 ? (1u << (8 * nb)) - 1u : 0u);
+      const uint32_t m1 = nb >= 8 ? ~0u : (nb > 4 ? (1u << (8 * (nb - 4))) - 1u : 0u);
+      const uint32_t m2 = nb >= 12 ? ~0u : (nb > 8 ? (1u << (8 * (nb - 8))) - 1u : 0u);
+      const uint32_t m3 = nb >= 16 ? ~0u : (nb > 12 ? (1u << (8 * (nb - 12))) - 1u : 0u);
+      uint4 o;
+      o.x = (v.x ^ ks[4 * q + 0]) & m0;
+      o.y = (v.y ^ ks[4 * q + 1]) & m1;
+      o.z = (v.z ^ ks[4 * q + 2]) & m2;
+      o.w = (v.w ^ ks[4 * q + 3]) & m3;
+      if (DECRYPT) poly_block(p, v.x, v.y, v.z, v.w);
+      else poly_block(p, o.x, o.y, o.z, o.w);
+      store16<VEC>(dst + 16 * q, o, nb);
+    }
+  }
+  // length block LE64(ad_len) || LE64(len)
+  poly_block(p, ad_len, 0u, len, 0u);
+  uint32_t tag[4];
+  poly_final(p, tag);
+  if (!DECRYPT) {
+    store16<VEC>(out + len, make_uint4(tag[0], tag[1], tag[2], tag[3]), 16);
+    return true;
+  }
+  const uint4 want = load16<VEC>(in + len, 16);
+  const uint32_t diff = (want.x ^ tag[0]) | (want.y ^ tag[1]) |
+                        (want.z ^ tag[2]) | (want.w ^ tag[3]);
+  if (diff == 0u) return true;
+  // Tag mismatch (rare, divergent).  In place: XOR the keystream back so
+  // the ciphertext is exactly as it was.  Out of place: zero the output.
+  const bool in_place = (in == out);
+  for (uint32_t off = 0; off < len; off += 64u) {
+    uint32_t ks[16];
+    if (in_place) chacha20_block(k, 1u + (off >> 6), n_lo, n_hi, ks);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int m = (int)(len - off) - 16 * q;
+      if (m <= 0) break;
+      const int nb = m >= 16 ? 16 : m;
+      uint4 o = make_uint4(0u, 0u, 0u, 0u);
+      if (in_place) {
+        const uint4 v = load16<VEC>(out + off + 16 * q, nb);
+        o = make_uint4(v.x ^ ks[4 * q + 0], v.y ^ ks[4 * q + 1],
+                       v.z ^ ks[4 * q + 2], v.w ^ ks[4 * q + 3]);
+      }
+      store16<VEC>(out + off + 16 * q, o, nb);
+    }
+  }
+  return false;
+}
+
+}  // namespace noise_amd

@@ -1,0 +1,483 @@
+// noise_gpu_api.hip -- the C ABI (include/noise_gpu.h) over the gfx950
+// kernels.  Argument checks, launches, and the host-buffer entry points
+// (pinned staging for single records; chunked, multi-stream pipelines for
+// host-resident batches).  Nothing here computes ChaCha20 or Poly1305:
+// every record goes through the HIP kernels, and without a gfx950 device
+// every entry point fails with NOISE_GPU_E_NODEV / NOISE_GPU_E_HIP.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <string>
+
+#include "launchers.hpp"
+#include "noise_gpu.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int hip_fail(hipError_t e, const char *what) {
+  g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+  return NOISE_GPU_E_HIP;
+}
+
+#define HIP_TRY(expr)                                  \
+  do {                                                 \
+    hipError_t e_ = (expr);                            \
+    if (e_ != hipSuccess) return hip_fail(e_, #expr);  \
+  } while (0)
+
+// Is a gfx950 device current?  Cached per thread and device.
+int check_device() {
+  thread_local int cached_dev = -1, cached_ok = 0;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+    g_last_error = "no HIP device visible";
+    return NOISE_GPU_E_NODEV;
+  }
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  if (dev == cached_dev) return cached_ok ? NOISE_GPU_OK : NOISE_GPU_E_NODEV;
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, dev));
+  cached_dev = dev;
+  cached_ok = std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+  if (!cached_ok) {
+    g_last_error = std::string("device is ") + prop.gcnArchName +
+                   ", this engine is built for gfx950 only";
+    return NOISE_GPU_E_NODEV;
+  }
+  return NOISE_GPU_OK;
+}
+
+void key_words(const uint8_t *key, uint32_t w[8]) { std::memcpy(w, key, 32); }
+
+int arg_fail(const char *msg) {
+  g_last_error = msg;
+  return NOISE_GPU_E_ARG;
+}
+
+// Validate a uniform batch.  enc: in = len-byte records, out = len+16.
+int check_uniform(bool decrypt, const void *in, uint64_t in_stride,
+                  const void *out, uint64_t out_stride, uint32_t len,
+                  const void *ad, uint32_t ad_len, const void *status,
+                  uint64_t nrec) {
+  if (nrec == 0) return NOISE_GPU_OK;
+  const uint64_t in_rec = decrypt ? (uint64_t)len + 16 : len;
+  const uint64_t out_rec = decrypt ? len : (uint64_t)len + 16;
+  if (!in || !out) return arg_fail("null record buffer");
+  if ((nrec > 1 && in_stride < in_rec) || (nrec > 1 && out_stride < out_rec))
+    return arg_fail("record stride smaller than the record");
+  if (in == out && in_stride != out_stride)
+    return arg_fail("in-place batches need equal strides");
+  if (in == out && nrec > 1 && in_stride < (uint64_t)len + 16)
+    return arg_fail("in-place stride must hold len+16 bytes");
+  if (ad_len && !ad) return arg_fail("ad_len > 0 with null ad");
+  if (decrypt && !status) return arg_fail("null status buffer");
+  return NOISE_GPU_OK;
+}
+
+// Per-thread staging for the synchronous host-buffer entry points.
+struct Staging {
+  int dev = -1;
+  hipStream_t stream = nullptr;
+  uint8_t *d = nullptr, *h = nullptr;
+  size_t cap = 0;
+  ~Staging() {
+    if (d) (void)hipFree(d);
+    if (h) (void)hipHostFree(h);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+  int reserve(size_t bytes) {
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    if (cur != dev) {  // device switched: drop the old device's resources
+      if (d) (void)hipFree(d);
+      if (stream) (void)hipStreamDestroy(stream);
+      d = nullptr; stream = nullptr; cap = 0; dev = cur;
+      HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    }
+    if (bytes <= cap) return NOISE_GPU_OK;
+    size_t want = cap ? cap : 4096;
+    while (want < bytes) want *= 2;
+    if (d) (void)hipFree(d);
+    if (h) (void)hipHostFree(h);
+    d = nullptr; h = nullptr; cap = 0;
+    HIP_TRY(hipMalloc(&d, want));
+    HIP_TRY(hipHostMalloc(&h, want, hipHostMallocDefault));
+    cap = want;
+    return NOISE_GPU_OK;
+  }
+};
+thread_local Staging g_stage;
+
+inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+
+}  // namespace
+
+extern "C" {
+
+const char *noise_gpu_version(void) { return "noise-mi355x 0.1.0 gfx950"; }
+
+const char *noise_gpu_strerror(int status) {
+  switch (status) {
+    case NOISE_GPU_OK: return "ok";
+    case NOISE_GPU_E_NONCE: return "Nonce limit has been exceeded!";
+    case NOISE_GPU_E_MAC: return "Invalid MAC";
+    case NOISE_GPU_E_ARG: return "invalid argument";
+    case NOISE_GPU_E_HIP: return "HIP runtime error";
+    case NOISE_GPU_E_NODEV: return "no gfx950 device";
+    default: return "unknown status";
+  }
+}
+
+const char *noise_gpu_last_error(void) { return g_last_error.c_str(); }
+
+int noise_gpu_device_count(int *count) {
+  if (!count) return arg_fail("null count");
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *count = n;
+  return NOISE_GPU_OK;
+}
+
+int noise_gpu_encrypt_uniform(const uint8_t h_key[32], uint64_t nonce0,
+                              const uint8_t *d_in, uint64_t in_stride,
+                              uint8_t *d_out, uint64_t out_stride,
+                              uint32_t len, const uint8_t *d_ad,
+                              uint64_t ad_stride, uint32_t ad_len,
+                              uint64_t nrec, void *stream) {
+  if (!h_key) return arg_fail("null key");
+  int rc = check_uniform(false, d_in, in_stride, d_out, out_stride, len, d_ad,
+                         ad_len, nullptr, nrec);
+  if (rc || nrec == 0) return rc;
+  if ((rc = check_device())) return rc;
+  uint32_t k[8];
+  key_words(h_key, k);
+  HIP_TRY(noise_amd::launch_aead_uniform(false, k, nonce0, d_in, in_stride,
+                                         d_out, out_stride, len, d_ad,
+                                         ad_stride, ad_len, nullptr, nrec,
+                                         (hipStream_t)stream));
+  return NOISE_GPU_OK;
+}
+
+int noise_gpu_decrypt_uniform(const uint8_t h_key[32], uint64_t nonce0,
+                              const uint8_t *d_in, uint64_t in_stride,
+                              uint8_t *d_out, uint64_t out_stride,
+                              uint32_t len, const uint8_t *d_ad,
+                              uint64_t ad_stride, uint32_t ad_len,
+                              uint8_t *d_status, uint64_t nrec, void *stream) {
+  if (!h_key) return arg_fail("null key");
+  int rc = check_uniform(true, d_in, in_stride, d_out, out_stride, len, d_ad,
+                         ad_len, d_status, nrec);
+  if (rc || nrec == 0) return rc;
+  if ((rc = check_device())) return rc;
+  uint32_t k[8];
+  key_words(h_key, k);
+  HIP_TRY(noise_amd::launch_aead_uniform(true, k, nonce0, d_in, in_stride,
+                                         d_out, out_stride, len, d_ad,
+                                         ad_stride, ad_len, d_status, nrec,
+                                         (hipStream_t)stream));
+  return NOISE_GPU_OK;
+}
+
+int noise_gpu_encrypt_records(const uint8_t *d_keys, uint32_t nkeys,
+                              const noise_gpu_record *d_recs, uint64_t nrec,
+                              const uint8_t *d_in, uint8_t *d_out,
+                              const uint8_t *d_ad, void *stream) {
+  if (nrec == 0) return NOISE_GPU_OK;
+  if (!d_keys || !nkeys || !d_recs || !d_in || !d_out)
+    return arg_fail("null key table / descriptors / buffers");
+  if (reinterpret_cast<uintptr_t>(d_keys) & 15u)
+    return arg_fail("key table must be 16-byte aligned");
+  int rc = check_device();
+  if (rc) return rc;
+  HIP_TRY(noise_amd::launch_aead_records(false, d_keys, nkeys, d_recs, nrec,
+                                         d_in, d_out, d_ad, nullptr,
+                                         (hipStream_t)stream));
+  return NOISE_GPU_OK;
+}
+
+int noise_gpu_decrypt_records(const uint8_t *d_keys, uint32_t nkeys,
+                              const noise_gpu_record *d_recs, uint64_t nrec,
+                              const uint8_t *d_in, uint8_t *d_out,
+                              const uint8_t *d_ad, uint8_t *d_status,
+                              void *stream) {
+  if (nrec == 0) return NOISE_GPU_OK;
+  if (!d_keys || !nkeys || !d_recs || !d_in || !d_out || !d_status)
+    return arg_fail("null key table / descriptors / buffers / status");
+  if (reinterpret_cast<uintptr_t>(d_keys) & 15u)
+    return arg_fail("key table must be 16-byte aligned");
+  int rc = check_device();
+  if (rc) return rc;
+  HIP_TRY(noise_amd::launch_aead_records(true, d_keys, nkeys, d_recs, nrec,
+                                         d_in, d_out, d_ad, d_status,
+                                         (hipStream_t)stream));
+  return NOISE_GPU_OK;
+}
+
+int noise_gpu_rekey_keys(uint8_t *d_keys, uint64_t nkeys, void *stream) {
+  if (nkeys == 0) return NOISE_GPU_OK;
+  if (!d_keys) return arg_fail("null key table");
+  if (reinterpret_cast<uintptr_t>(d_keys) & 15u)
+    return arg_fail("key table must be 16-byte aligned");
+  int rc = check_device();
+  if (rc) return rc;
+  HIP_TRY(noise_amd::launch_rekey(d_keys, nkeys, (hipStream_t)stream));
+  return NOISE_GPU_OK;
+}
+
+int noise_gpu_fill_synthetic(uint8_t *d_dst, uint64_t offset, uint64_t nbytes,
+                             uint64_t seed, void *stream) {
+  if (nbytes == 0) return NOISE_GPU_OK;
+  if (!d_dst) return arg_fail("null destination");
+  int rc = check_device();
+  if (rc) return rc;
+  HIP_TRY(noise_amd::launch_fill_synthetic(d_dst, offset, nbytes, seed,
+                                           (hipStream_t)stream));
+  return NOISE_GPU_OK;
+}
+
+// ---- synchronous host-buffer entry points (CipherState single records)
+// Device scratch layout: [ad | pad][record in | pad][record out][status]
+
+int noise_gpu_encrypt_host(const uint8_t h_key[32], uint64_t nonce,
+                           const uint8_t *h_ad, size_t ad_len, uint8_t *h_buf,
+                           size_t len) {
+  if (!h_key || !h_buf || (ad_len && !h_ad))
+    return arg_fail("null key / buffer / ad");
+  if (len > 0xffffffffull - 16 || ad_len > 0xffffffffull)
+    return arg_fail("record too large");
+  int rc = check_device();
+  if (rc) return rc;
+  const size_t ad_sz = align16(ad_len), rec_sz = align16(len + 16);
+  if ((rc = g_stage.reserve(ad_sz + rec_sz))) return rc;
+  Staging &s = g_stage;
+  std::memcpy(s.h, h_ad, ad_len);
+  std::memcpy(s.h + ad_sz, h_buf, len);
+  HIP_TRY(hipMemcpyAsync(s.d, s.h, ad_sz + len, hipMemcpyHostToDevice, s.stream));
+  uint32_t k[8];
+  key_words(h_key, k);
+  HIP_TRY(noise_amd::launch_aead_uniform(false, k, nonce, s.d + ad_sz, 0,
+                                         s.d + ad_sz, 0, (uint32_t)len, s.d, 0,
+                                         (uint32_t)ad_len, nullptr, 1, s.stream));
+  HIP_TRY(hipMemcpyAsync(s.h + ad_sz, s.d + ad_sz, len + 16, hipMemcpyDeviceToHost, s.stream));
+  HIP_TRY(hipStreamSynchronize(s.stream));
+  std::memcpy(h_buf, s.h + ad_sz, len + 16);
+  std::memset(s.h, 0, ad_sz + len + 16);  // plaintext/ciphertext hygiene
+  return NOISE_GPU_OK;
+}
+
+int noise_gpu_decrypt_host(const uint8_t h_key[32], uint64_t nonce,
+                           const uint8_t *h_ad, size_t ad_len, uint8_t *h_buf,
+                           size_t ct_len) {
+  if (!h_key || !h_buf || (ad_len && !h_ad))
+    return arg_fail("null key / buffer / ad");
+  if (ct_len < 16) {  // reference UB (noise.cpp:257); defined as bad MAC
+    g_last_error = "ciphertext shorter than the tag";
+    return NOISE_GPU_E_MAC;
+  }
+  if (ct_len > 0xffffffffull || ad_len > 0xffffffffull)
+    return arg_fail("record too large");
+  int rc = check_device();
+  if (rc) return rc;
+  const size_t len = ct_len - 16;
+  const size_t ad_sz = align16(ad_len), in_sz = align16(ct_len),
+               out_sz = align16(len);
+  if ((rc = g_stage.reserve(ad_sz + in_sz + out_sz + 16))) return rc;
+  Staging &s = g_stage;
+  uint8_t *d_in = s.d + ad_sz, *d_out = d_in + in_sz, *d_st = d_out + out_sz;
+  std::memcpy(s.h, h_ad, ad_len);
+  std::memcpy(s.h + ad_sz, h_buf, ct_len);
+  HIP_TRY(hipMemcpyAsync(s.d, s.h, ad_sz + ct_len, hipMemcpyHostToDevice, s.stream));
+  uint32_t k[8];
+  key_words(h_key, k);
+  HIP_TRY(noise_amd::launch_aead_uniform(true, k, nonce, d_in, 0, d_out, 0,
+                                         (uint32_t)len, s.d, 0,
+                                         (uint32_t)ad_len, d_st, 1, s.stream));
+  uint8_t *h_out = s.h + ad_sz + in_sz;
+  HIP_TRY(hipMemcpyAsync(h_out, d_out, out_sz + 16, hipMemcpyDeviceToHost, s.stream));
+  HIP_TRY(hipStreamSynchronize(s.stream));
+  const uint8_t st = h_out[out_sz];
+  if (st == NOISE_GPU_REC_OK) std::memcpy(h_buf, h_out, len);
+  std::memset(s.h, 0, ad_sz + in_sz + out_sz + 16);
+  if (st != NOISE_GPU_REC_OK) {
+    g_last_error = "Invalid MAC";
+    return NOISE_GPU_E_MAC;
+  }
+  return NOISE_GPU_OK;
+}
+
+int noise_gpu_rekey_host(uint8_t h_key[32]) {
+  if (!h_key) return arg_fail("null key");
+  int rc = check_device();
+  if (rc) return rc;
+  if ((rc = g_stage.reserve(32))) return rc;
+  Staging &s = g_stage;
+  std::memcpy(s.h, h_key, 32);
+  HIP_TRY(hipMemcpyAsync(s.d, s.h, 32, hipMemcpyHostToDevice, s.stream));
+  HIP_TRY(noise_amd::launch_rekey(s.d, 1, s.stream));
+  HIP_TRY(hipMemcpyAsync(s.h, s.d, 32, hipMemcpyDeviceToHost, s.stream));
+  HIP_TRY(hipStreamSynchronize(s.stream));
+  std::memcpy(h_key, s.h, 32);
+  std::memset(s.h, 0, 32);
+  return NOISE_GPU_OK;
+}
+
+// ---- host descriptor batches (CipherState::encrypt_batch/decrypt_batch)
+static int records_host(bool decrypt, const uint8_t *h_keys, uint32_t nkeys,
+                        const noise_gpu_record *h_recs, uint64_t nrec,
+                        const uint8_t *h_in, uint64_t in_bytes, uint8_t *h_out,
+                        uint64_t out_bytes, const uint8_t *h_ad,
+                        uint64_t ad_bytes, uint8_t *h_status) {
+  if (nrec == 0) return NOISE_GPU_OK;
+  if (!h_keys || !nkeys || !h_recs || (in_bytes && !h_in) ||
+      (out_bytes && !h_out) || (ad_bytes && !h_ad) || (decrypt && !h_status))
+    return arg_fail("null key table / descriptors / buffers");
+  for (uint64_t i = 0; i < nrec; ++i) {  // host-side bounds check of every record
+    const noise_gpu_record &r = h_recs[i];
+    const uint64_t in_len = decrypt ? (uint64_t)r.len + 16 : r.len;
+    const uint64_t out_len = decrypt ? r.len : (uint64_t)r.len + 16;
+    if (r.key_idx >= nkeys || r.in_off + in_len > in_bytes ||
+        r.out_off + out_len > out_bytes ||
+        (r.ad_len && r.ad_off + r.ad_len > ad_bytes))
+      return arg_fail("record descriptor out of range");
+  }
+  int rc = check_device();
+  if (rc) return rc;
+  const size_t o_keys = 0, o_recs = align16(32ull * nkeys),
+               o_in = o_recs + align16(sizeof(noise_gpu_record) * nrec),
+               o_out = o_in + align16(in_bytes), o_ad = o_out + align16(out_bytes),
+               o_st = o_ad + align16(ad_bytes), total = o_st + align16(nrec);
+  if ((rc = g_stage.reserve(total))) return rc;
+  Staging &s = g_stage;
+  std::memcpy(s.h + o_keys, h_keys, 32ull * nkeys);
+  std::memcpy(s.h + o_recs, h_recs, sizeof(noise_gpu_record) * nrec);
+  if (in_bytes) std::memcpy(s.h + o_in, h_in, in_bytes);
+  if (ad_bytes) std::memcpy(s.h + o_ad, h_ad, ad_bytes);
+  HIP_TRY(hipMemcpyAsync(s.d, s.h, o_out, hipMemcpyHostToDevice, s.stream));
+  if (ad_bytes)
+    HIP_TRY(hipMemcpyAsync(s.d + o_ad, s.h + o_ad, ad_bytes, hipMemcpyHostToDevice, s.stream));
+  HIP_TRY(noise_amd::launch_aead_records(
+      decrypt, s.d + o_keys, nkeys,
+      reinterpret_cast<const noise_gpu_record *>(s.d + o_recs), nrec, s.d + o_in,
+      s.d + o_out, s.d + o_ad, decrypt ? s.d + o_st : nullptr, s.stream));
+  HIP_TRY(hipMemcpyAsync(s.h + o_out, s.d + o_out, o_st + nrec - o_out,
+                         hipMemcpyDeviceToHost, s.stream));
+  HIP_TRY(hipStreamSynchronize(s.stream));
+  if (out_bytes) std::memcpy(h_out, s.h + o_out, out_bytes);
+  if (decrypt) std::memcpy(h_status, s.h + o_st, nrec);
+  std::memset(s.h, 0, total);
+  return NOISE_GPU_OK;
+}
+
+int noise_gpu_encrypt_records_host(const uint8_t *h_keys, uint32_t nkeys,
+                                   const noise_gpu_record *h_recs,
+                                   uint64_t nrec, const uint8_t *h_in,
+                                   uint64_t in_bytes, uint8_t *h_out,
+                                   uint64_t out_bytes, const uint8_t *h_ad,
+                                   uint64_t ad_bytes) {
+  return records_host(false, h_keys, nkeys, h_recs, nrec, h_in, in_bytes,
+                      h_out, out_bytes, h_ad, ad_bytes, nullptr);
+}
+
+int noise_gpu_decrypt_records_host(const uint8_t *h_keys, uint32_t nkeys,
+                                   const noise_gpu_record *h_recs,
+                                   uint64_t nrec, const uint8_t *h_in,
+                                   uint64_t in_bytes, uint8_t *h_out,
+                                   uint64_t out_bytes, const uint8_t *h_ad,
+                                   uint64_t ad_bytes, uint8_t *h_status) {
+  return records_host(true, h_keys, nkeys, h_recs, nrec, h_in, in_bytes, h_out,
+                      out_bytes, h_ad, ad_bytes, h_status);
+}
+
+// ---- host-resident uniform batches: chunked 3-stream pipeline ----------
+static int uniform_host(bool decrypt, const uint8_t h_key[32], uint64_t nonce0,
+                        const uint8_t *h_in, uint64_t in_stride, uint8_t *h_out,
+                        uint64_t out_stride, uint32_t len, uint8_t *h_status,
+                        uint64_t nrec, double *seconds) {
+  if (!h_key) return arg_fail("null key");
+  int rc = check_uniform(decrypt, h_in, in_stride, h_out, out_stride, len,
+                         nullptr, 0, decrypt ? (const void *)h_status : h_in,
+                         nrec);
+  if (rc) return rc;
+  if (h_in == h_out) return arg_fail("host batches must be out-of-place");
+  if (nrec == 0) {
+    if (seconds) *seconds = 0;
+    return NOISE_GPU_OK;
+  }
+  if ((rc = check_device())) return rc;
+  const uint64_t in_rec = decrypt ? (uint64_t)len + 16 : len;
+  const uint64_t out_rec = decrypt ? len : (uint64_t)len + 16;
+  // device chunks are packed (stride = record size); ~32 MiB per chunk
+  const uint64_t per = std::max<uint64_t>(1, (32ull << 20) / (in_rec + out_rec + 1));
+  constexpr int kDepth = 3;
+  hipStream_t st[kDepth] = {};
+  uint8_t *d_in[kDepth] = {}, *d_out[kDepth] = {}, *d_stat[kDepth] = {};
+  uint32_t k[8];
+  key_words(h_key, k);
+  auto cleanup = [&]() {
+    for (int i = 0; i < kDepth; ++i) {
+      if (st[i]) (void)hipStreamSynchronize(st[i]);
+      if (d_in[i]) (void)hipFree(d_in[i]);
+      if (d_out[i]) (void)hipFree(d_out[i]);
+      if (d_stat[i]) (void)hipFree(d_stat[i]);
+      if (st[i]) (void)hipStreamDestroy(st[i]);
+    }
+  };
+  hipError_t e = hipSuccess;
+  for (int i = 0; i < kDepth && e == hipSuccess; ++i) {
+    e = hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&d_in[i], per * in_rec);
+    if (e == hipSuccess) e = hipMalloc(&d_out[i], per * out_rec);
+    if (e == hipSuccess && decrypt) e = hipMalloc(&d_stat[i], per);
+  }
+  if (e != hipSuccess) {
+    cleanup();
+    return hip_fail(e, "pipeline setup");
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t first = 0, c = 0; first < nrec && e == hipSuccess; first += per, ++c) {
+    const uint64_t n = std::min(per, nrec - first);
+    const int b = (int)(c % kDepth);
+    e = hipMemcpy2DAsync(d_in[b], in_rec, h_in + first * in_stride, in_stride,
+                         in_rec, n, hipMemcpyHostToDevice, st[b]);
+    if (e == hipSuccess)
+      e = noise_amd::launch_aead_uniform(decrypt, k, nonce0 + first, d_in[b],
+                                         in_rec, d_out[b], out_rec, len,
+                                         nullptr, 0, 0, d_stat[b], n, st[b]);
+    if (e == hipSuccess)
+      e = hipMemcpy2DAsync(h_out + first * out_stride, out_stride, d_out[b],
+                           out_rec, out_rec, n, hipMemcpyDeviceToHost, st[b]);
+    if (e == hipSuccess && decrypt)
+      e = hipMemcpyAsync(h_status + first, d_stat[b], n, hipMemcpyDeviceToHost, st[b]);
+  }
+  for (int i = 0; i < kDepth && e == hipSuccess; ++i) e = hipStreamSynchronize(st[i]);
+  const auto t1 = std::chrono::steady_clock::now();
+  cleanup();
+  if (e != hipSuccess) return hip_fail(e, "host pipeline");
+  if (seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
+  return NOISE_GPU_OK;
+}
+
+int noise_gpu_encrypt_uniform_host(const uint8_t h_key[32], uint64_t nonce0,
+                                   const uint8_t *h_in, uint64_t in_stride,
+                                   uint8_t *h_out, uint64_t out_stride,
+                                   uint32_t len, uint64_t nrec,
+                                   double *seconds) {
+  return uniform_host(false, h_key, nonce0, h_in, in_stride, h_out, out_stride,
+                      len, nullptr, nrec, seconds);
+}
+
+int noise_gpu_decrypt_uniform_host(const uint8_t h_key[32], uint64_t nonce0,
+                                   const uint8_t *h_in, uint64_t in_stride,
+                                   uint8_t *h_out, uint64_t out_stride,
+                                   uint32_t len, uint8_t *h_status,
+                                   uint64_t nrec, double *seconds) {
+  return uniform_host(true, h_key, nonce0, h_in, in_stride, h_out, out_stride,
+                      len, h_status, nrec, seconds);
+}
+
+}  // extern "C"

@@ -1,0 +1,200 @@
+"""ctypes binding of the MI355X Noise ChaChaPoly engine (include/noise_gpu.h).
+
+The product is the C ABI in noise-cpp_amd/lib/libnoise_amd.so (HIP kernels for
+gfx950) and the C++20 noise::CipherState over it.  This module is the thin
+Python view used by tests/, bench.py and __graft_entry__.py: it passes device
+pointers (torch tensors on the GPU are used only as HBM allocations) and
+streams straight through to the C ABI.  There is no Python or CPU compute
+path: if the shared library is missing, load() raises.
+"""
+import ctypes
+import os
+import re
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", "..", ".."))
+PKG = os.path.join(ROOT, "noise-cpp_amd")
+LIB_PATH = os.path.join(PKG, "lib", "libnoise_amd.so")
+HEADER = os.path.join(ROOT, "include", "noise_gpu.h")
+
+OK, E_NONCE, E_MAC, E_ARG, E_HIP, E_NODEV = 0, 1, 2, 3, 4, 5
+REC_OK, REC_BAD_MAC = 0, 1
+NONCE_LIMIT = (1 << 64) - 2  # noise.cpp:398 refuses n == 2^64-2
+
+
+class Record(ctypes.Structure):
+    """noise_gpu_record (include/noise_gpu.h)."""
+    _fields_ = [("in_off", ctypes.c_uint64), ("out_off", ctypes.c_uint64),
+                ("nonce", ctypes.c_uint64), ("ad_off", ctypes.c_uint64),
+                ("len", ctypes.c_uint32), ("ad_len", ctypes.c_uint32),
+                ("key_idx", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+RECORD_DTYPE = None  # numpy structured dtype, built lazily
+
+
+def record_dtype():
+    global RECORD_DTYPE
+    if RECORD_DTYPE is None:
+        import numpy as np
+        RECORD_DTYPE = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("nonce", "<u8"),
+                                 ("ad_off", "<u8"), ("len", "<u4"), ("ad_len", "<u4"),
+                                 ("key_idx", "<u4"), ("reserved", "<u4")])
+        assert RECORD_DTYPE.itemsize == ctypes.sizeof(Record) == 48
+    return RECORD_DTYPE
+
+
+class NoiseGpuError(RuntimeError):
+    def __init__(self, code, what):
+        super().__init__("%s (status %d): %s" % (what, code, _lib.noise_gpu_last_error().decode()
+                                                if _lib else ""))
+        self.code = code
+
+
+_lib = None
+u8p, u64, u32, vp = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p
+
+
+def declared_symbols():
+    """Function names declared in include/noise_gpu.h."""
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^(?:int|const char \*)\s*(noise_gpu_\w+)\s*\(", text, re.M)))
+
+
+def load(path=LIB_PATH):
+    """Load the engine library (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise FileNotFoundError("libnoise_amd.so not built (%s); run __graft_entry__.build()" % path)
+    lib = ctypes.CDLL(path)
+    sig = {
+        "noise_gpu_version": (ctypes.c_char_p, []),
+        "noise_gpu_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+        "noise_gpu_last_error": (ctypes.c_char_p, []),
+        "noise_gpu_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+        "noise_gpu_encrypt_uniform": (ctypes.c_int, [ctypes.c_char_p, u64, u8p, u64, u8p, u64, u32,
+                                                     u8p, u64, u32, u64, vp]),
+        "noise_gpu_decrypt_uniform": (ctypes.c_int, [ctypes.c_char_p, u64, u8p, u64, u8p, u64, u32,
+                                                     u8p, u64, u32, u8p, u64, vp]),
+        "noise_gpu_encrypt_records": (ctypes.c_int, [u8p, u32, u8p, u64, u8p, u8p, u8p, vp]),
+        "noise_gpu_decrypt_records": (ctypes.c_int, [u8p, u32, u8p, u64, u8p, u8p, u8p, u8p, vp]),
+        "noise_gpu_rekey_keys": (ctypes.c_int, [u8p, u64, vp]),
+        "noise_gpu_encrypt_host": (ctypes.c_int, [ctypes.c_char_p, u64, u8p, ctypes.c_size_t,
+                                                  u8p, ctypes.c_size_t]),
+        "noise_gpu_decrypt_host": (ctypes.c_int, [ctypes.c_char_p, u64, u8p, ctypes.c_size_t,
+                                                  u8p, ctypes.c_size_t]),
+        "noise_gpu_rekey_host": (ctypes.c_int, [u8p]),
+        "noise_gpu_encrypt_records_host": (ctypes.c_int, [u8p, u32, u8p, u64, u8p, u64, u8p, u64,
+                                                          u8p, u64]),
+        "noise_gpu_decrypt_records_host": (ctypes.c_int, [u8p, u32, u8p, u64, u8p, u64, u8p, u64,
+                                                          u8p, u64, u8p]),
+        "noise_gpu_encrypt_uniform_host": (ctypes.c_int, [ctypes.c_char_p, u64, u8p, u64, u8p, u64,
+                                                          u32, u64, ctypes.POINTER(ctypes.c_double)]),
+        "noise_gpu_decrypt_uniform_host": (ctypes.c_int, [ctypes.c_char_p, u64, u8p, u64, u8p, u64,
+                                                          u32, u8p, u64,
+                                                          ctypes.POINTER(ctypes.c_double)]),
+        "noise_gpu_fill_synthetic": (ctypes.c_int, [u8p, u64, u64, u64, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype, fn.argtypes = res, args
+    _lib = lib
+    return lib
+
+
+def _check(rc, what):
+    if rc != OK:
+        raise NoiseGpuError(rc, what)
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(stream):
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream()
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+def _key(key):
+    key = bytes(key)
+    if len(key) != 32:
+        raise ValueError("key must be 32 bytes")
+    return key
+
+
+# ---- device-resident batches (torch uint8 CUDA tensors as HBM buffers) ----
+def encrypt_uniform(key, nonce0, d_in, in_stride, d_out, out_stride, length, nrec,
+                    d_ad=None, ad_stride=0, ad_len=0, stream=None, in_offset=0, out_offset=0):
+    lib = load()
+    rc = lib.noise_gpu_encrypt_uniform(_key(key), nonce0 % (1 << 64),
+                                       ctypes.c_void_p(d_in.data_ptr() + in_offset), in_stride,
+                                       ctypes.c_void_p(d_out.data_ptr() + out_offset), out_stride,
+                                       length, _ptr(d_ad), ad_stride, ad_len, nrec, _stream(stream))
+    _check(rc, "noise_gpu_encrypt_uniform")
+
+
+def decrypt_uniform(key, nonce0, d_in, in_stride, d_out, out_stride, length, d_status, nrec,
+                    d_ad=None, ad_stride=0, ad_len=0, stream=None, in_offset=0, out_offset=0):
+    lib = load()
+    rc = lib.noise_gpu_decrypt_uniform(_key(key), nonce0 % (1 << 64),
+                                       ctypes.c_void_p(d_in.data_ptr() + in_offset), in_stride,
+                                       ctypes.c_void_p(d_out.data_ptr() + out_offset), out_stride,
+                                       length, _ptr(d_ad), ad_stride, ad_len, _ptr(d_status), nrec,
+                                       _stream(stream))
+    _check(rc, "noise_gpu_decrypt_uniform")
+
+
+def encrypt_records(d_keys, nkeys, d_recs, nrec, d_in, d_out, d_ad=None, stream=None):
+    rc = load().noise_gpu_encrypt_records(_ptr(d_keys), nkeys, _ptr(d_recs), nrec, _ptr(d_in),
+                                          _ptr(d_out), _ptr(d_ad), _stream(stream))
+    _check(rc, "noise_gpu_encrypt_records")
+
+
+def decrypt_records(d_keys, nkeys, d_recs, nrec, d_in, d_out, d_status, d_ad=None, stream=None):
+    rc = load().noise_gpu_decrypt_records(_ptr(d_keys), nkeys, _ptr(d_recs), nrec, _ptr(d_in),
+                                          _ptr(d_out), _ptr(d_ad), _ptr(d_status), _stream(stream))
+    _check(rc, "noise_gpu_decrypt_records")
+
+
+def rekey_keys(d_keys, nkeys, stream=None):
+    _check(load().noise_gpu_rekey_keys(_ptr(d_keys), nkeys, _stream(stream)), "noise_gpu_rekey_keys")
+
+
+def fill_synthetic(d_dst, nbytes, seed, offset=0, stream=None, dst_offset=0):
+    rc = load().noise_gpu_fill_synthetic(ctypes.c_void_p(d_dst.data_ptr() + dst_offset), offset,
+                                         nbytes, seed, _stream(stream))
+    _check(rc, "noise_gpu_fill_synthetic")
+
+
+# ---- host-buffer entry points (CipherState single-record path) ------------
+def encrypt_host(key, nonce, ad, plaintext):
+    """ENCRYPT(k, n, ad, pt) through the GPU; returns ct || tag (bytes)."""
+    buf = ctypes.create_string_buffer(bytes(plaintext), len(plaintext) + 16)
+    adb = bytes(ad)
+    rc = load().noise_gpu_encrypt_host(_key(key), nonce, adb or None, len(adb), buf, len(plaintext))
+    _check(rc, "noise_gpu_encrypt_host")
+    return buf.raw
+
+
+def decrypt_host(key, nonce, ad, ciphertext):
+    """DECRYPT through the GPU; returns plaintext or raises NoiseGpuError(E_MAC)."""
+    ct = bytes(ciphertext)
+    buf = ctypes.create_string_buffer(ct, max(len(ct), 1))
+    adb = bytes(ad)
+    rc = load().noise_gpu_decrypt_host(_key(key), nonce, adb or None, len(adb), buf, len(ct))
+    _check(rc, "noise_gpu_decrypt_host")
+    return buf.raw[:len(ct) - 16]
+
+
+def rekey_host(key):
+    buf = ctypes.create_string_buffer(_key(key), 32)
+    _check(load().noise_gpu_rekey_host(buf), "noise_gpu_rekey_host")
+    return buf.raw
+
+
+def version():
+    return load().noise_gpu_version().decode()

@@ -1,0 +1,78 @@
+"""CPU: the C-ABI library builds, loads, exports every symbol include/noise_gpu.h
+declares, validates arguments before touching a device, and fails loudly
+(no CPU fallback) when no gfx950 device is present."""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+import noise_amd
+
+ROOT = noise_amd.ROOT
+
+
+def test_library_exports_every_declared_symbol():
+    lib = noise_amd.load()
+    names = noise_amd.declared_symbols()
+    assert len(names) >= 17
+    for name in names:
+        assert hasattr(lib, name), name
+    nm = subprocess.run(["nm", "-D", "--defined-only", noise_amd.LIB_PATH], capture_output=True,
+                        text=True, check=True).stdout
+    exported = {line.split()[-1] for line in nm.splitlines() if " T " in line}
+    assert set(names) <= exported
+
+
+def test_library_does_not_link_the_oracle():
+    out = subprocess.run(["ldd", noise_amd.LIB_PATH], capture_output=True, text=True).stdout
+    assert "oracle" not in out and "noise_ref" not in out
+    nm = subprocess.run(["nm", "-D", noise_amd.LIB_PATH], capture_output=True, text=True).stdout
+    assert "oracle_" not in nm and "crypto_aead" not in nm
+
+
+def test_status_strings():
+    lib = noise_amd.load()
+    assert lib.noise_gpu_strerror(noise_amd.E_MAC) == b"Invalid MAC"
+    assert lib.noise_gpu_strerror(noise_amd.E_NONCE) == b"Nonce limit has been exceeded!"
+    assert lib.noise_gpu_version().startswith(b"noise-mi355x")
+
+
+def test_argument_validation_precedes_device():
+    lib = noise_amd.load()
+    key = bytes(32)
+    buf = ctypes.c_void_p(0x10000)
+    # null buffers
+    assert lib.noise_gpu_encrypt_uniform(key, 0, None, 64, buf, 80, 64, None, 0, 0, 4, None) == noise_amd.E_ARG
+    # output stride smaller than len + 16
+    assert lib.noise_gpu_encrypt_uniform(key, 0, buf, 64, ctypes.c_void_p(0x90000), 64, 64, None, 0, 0, 4,
+                                         None) == noise_amd.E_ARG
+    # in-place with unequal strides
+    assert lib.noise_gpu_encrypt_uniform(key, 0, buf, 80, buf, 96, 64, None, 0, 0, 4, None) == noise_amd.E_ARG
+    # ad_len without ad
+    assert lib.noise_gpu_encrypt_uniform(key, 0, buf, 64, ctypes.c_void_p(0x90000), 80, 64, None, 0, 8, 4,
+                                         None) == noise_amd.E_ARG
+    # decrypt without status
+    assert lib.noise_gpu_decrypt_uniform(key, 0, buf, 80, ctypes.c_void_p(0x90000), 64, 64, None, 0, 0,
+                                         None, 4, None) == noise_amd.E_ARG
+    # empty batches are no-ops, even without a device
+    assert lib.noise_gpu_encrypt_uniform(key, 0, None, 0, None, 0, 0, None, 0, 0, 0, None) == noise_amd.OK
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a GPU is visible")
+def test_no_device_fails_loudly():
+    with pytest.raises(noise_amd.NoiseGpuError) as e:
+        noise_amd.encrypt_host(bytes(range(32)), 0, b"", b"hello")
+    assert e.value.code == noise_amd.E_NODEV
+    lib = noise_amd.load()
+    assert lib.noise_gpu_rekey_host(ctypes.create_string_buffer(32)) == noise_amd.E_NODEV
+
+
+def test_cipherstate_host_rules():
+    """noise::CipherState rules that run before any device call: spec
+    has_key, the 2^64-2 nonce limit (noise.cpp:398), 40-byte layout."""
+    exe = os.path.join(ROOT, "noise-cpp_amd", "bin", "cipherstate_test")
+    assert os.path.exists(exe), "build() first"
+    r = subprocess.run([exe, "--host-only"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "PASSED" in r.stdout

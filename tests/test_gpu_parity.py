@@ -1,0 +1,324 @@
+"""GPU parity: the gfx950 kernels, called through the C ABI, against the CPU
+oracle and the golden records from the reference's tests/vectors.
+Bit-exact everywhere (integer/byte work)."""
+import hashlib
+import os
+import random
+import subprocess
+
+import numpy as np
+import pytest
+
+import noise_amd
+import oracle_lib
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+SEED = 0x4E4F495345  # splitmix64 seed of BASELINE config 2
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    noise_amd.load()
+    torch.cuda.set_device(0)
+
+
+def dev(b):
+    """bytes/np.uint8 -> uint8 CUDA tensor (at least 1 element)."""
+    a = np.frombuffer(bytes(b), dtype=np.uint8) if not isinstance(b, np.ndarray) else b
+    if a.size == 0:
+        a = np.zeros(1, dtype=np.uint8)
+    return torch.from_numpy(a.copy()).cuda()
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy().tobytes()
+
+
+def pack_records(recs, decrypt=False, align=16):
+    """Lay golden-style records out in buffers + descriptors (records kernel)."""
+    keys, desc, inb, adb = [], [], bytearray(), bytearray()
+    out_off = 0
+    for i, r in enumerate(recs):
+        data = r["ct"] if decrypt else r["pt"]
+        L = len(r["pt"])
+        in_off = len(inb)
+        inb += data + bytes(-len(data) % align)
+        ad_off = len(adb)
+        adb += r["ad"] + bytes(-len(r["ad"]) % align)
+        out_len = L if decrypt else L + 16
+        desc.append((in_off, out_off, r["nonce"], ad_off, L, len(r["ad"]), i, 0))
+        out_off += out_len + (-out_len % align)
+        keys.append(r["key"])
+    d = np.array(desc, dtype=noise_amd.record_dtype())
+    return (b"".join(keys), d, bytes(inb), bytes(adb), out_off)
+
+
+def run_records(recs, decrypt=False):
+    keys, d, inb, adb, out_bytes = pack_records(recs, decrypt)
+    d_keys, d_desc = dev(keys), dev(d.view(np.uint8))
+    d_in, d_ad = dev(inb), dev(adb)
+    d_out = torch.zeros(max(out_bytes, 1), dtype=torch.uint8, device="cuda")
+    if decrypt:
+        d_st = torch.full((len(recs),), 7, dtype=torch.uint8, device="cuda")
+        noise_amd.decrypt_records(d_keys, len(recs), d_desc, len(recs), d_in, d_out, d_st, d_ad)
+        st = host(d_st)
+    else:
+        noise_amd.encrypt_records(d_keys, len(recs), d_desc, len(recs), d_in, d_out, d_ad)
+        st = None
+    out = host(d_out)
+    res = []
+    for i, r in enumerate(recs):
+        L = len(r["pt"])
+        o = int(d[i]["out_off"])
+        res.append(out[o:o + (L if decrypt else L + 16)])
+    return res, st
+
+
+@pytest.mark.parametrize("kind", ["transport", "handshake"])
+def test_golden_records_kernel(golden, kind):
+    recs = golden[kind]
+    enc, _ = run_records(recs)
+    bad = [r["vector"] for r, c in zip(recs, enc) if c != r["ct"]]
+    assert not bad, "%d/%d mismatches, first %s" % (len(bad), len(recs), bad[:3])
+    dec, st = run_records(recs, decrypt=True)
+    assert set(st) == {0}
+    assert all(p == r["pt"] for r, p in zip(recs, dec))
+
+
+def test_golden_single_record_host_path(golden):
+    for r in golden["transport"][::7] + golden["handshake"][::11]:
+        assert noise_amd.encrypt_host(r["key"], r["nonce"], r["ad"], r["pt"]) == r["ct"]
+        assert noise_amd.decrypt_host(r["key"], r["nonce"], r["ad"], r["ct"]) == r["pt"]
+
+
+def test_kats_and_rekey(oracle):
+    for k, n, ad, pt, ct in (oracle_lib.KAT_K1, oracle_lib.KAT_K2, oracle_lib.KAT_K3):
+        assert noise_amd.encrypt_host(bytes.fromhex(k), n, bytes.fromhex(ad),
+                                      bytes.fromhex(pt)).hex() == ct
+    for n, (head, tag, digest) in oracle_lib.KAT_K5.items():
+        out = noise_amd.encrypt_host(bytes(range(32)), n, b"", oracle_lib.k5_plaintext())
+        assert out[:16].hex() == head and out[1024:].hex() == tag
+        assert hashlib.blake2b(out[:1024], digest_size=32).hexdigest() == digest
+    assert noise_amd.rekey_host(bytes(32)).hex() == oracle_lib.KAT_K4_REKEY_ZERO
+    rng = random.Random(3)
+    keys = [rng.randbytes(32) for _ in range(1000)]
+    d_keys = dev(b"".join(keys))
+    noise_amd.rekey_keys(d_keys, len(keys))
+    got = host(d_keys)
+    assert all(got[32 * i:32 * i + 32] == oracle.rekey(k) for i, k in enumerate(keys))
+
+
+LENGTHS = [0, 1, 3, 15, 16, 17, 31, 32, 48, 63, 64, 65, 100, 127, 128, 129, 255, 256, 1000,
+           1023, 1024, 1025, 1040, 4096, 65519]
+
+
+@pytest.mark.parametrize("length", LENGTHS)
+@pytest.mark.parametrize("layout", ["packed16", "odd"])
+def test_uniform_lengths_vs_oracle(oracle, length, layout):
+    rng = random.Random(length * 31 + len(layout))
+    nrec = 37 if length <= 4096 else 5
+    key = rng.randbytes(32)
+    n0 = rng.getrandbits(64)
+    if layout == "packed16":
+        in_stride = (length + 15) & ~15
+        out_stride = (length + 16 + 15) & ~15
+    else:  # strides and base offsets that break 16-byte alignment
+        in_stride, out_stride = length + 3, length + 16 + 5
+    in_off, out_off = (0, 0) if layout == "packed16" else (1, 7)
+    pt = np.frombuffer(rng.randbytes(in_stride * nrec + 8), dtype=np.uint8)
+    d_in = dev(pt)
+    d_out = torch.zeros(out_stride * nrec + 16, dtype=torch.uint8, device="cuda")
+    noise_amd.encrypt_uniform(key, n0, d_in, in_stride, d_out, out_stride, length, nrec,
+                              in_offset=in_off, out_offset=out_off)
+    out = host(d_out)
+    for i in range(nrec):
+        p = pt[in_off + i * in_stride: in_off + i * in_stride + length].tobytes()
+        want = oracle.encrypt(key, n0 + i, b"", p)
+        assert out[out_off + i * out_stride: out_off + i * out_stride + length + 16] == want, i
+    # decrypt back (out-of-place) and compare
+    d_pt = torch.zeros(in_stride * nrec + 16, dtype=torch.uint8, device="cuda")
+    d_st = torch.full((nrec,), 9, dtype=torch.uint8, device="cuda")
+    noise_amd.decrypt_uniform(key, n0, d_out, out_stride, d_pt, in_stride, length, d_st, nrec,
+                              in_offset=out_off, out_offset=in_off)
+    assert set(host(d_st)) == {0}
+    back = host(d_pt)
+    for i in range(nrec):
+        s = in_off + i * in_stride
+        assert back[s:s + length] == pt[s:s + length].tobytes()
+
+
+@pytest.mark.parametrize("ad_mode", ["shared", "per_record"])
+def test_uniform_with_ad(oracle, ad_mode):
+    rng = random.Random(11)
+    nrec, length, ad_len = 50, 200, 64
+    key, n0 = rng.randbytes(32), 5
+    ad = rng.randbytes(ad_len * (nrec if ad_mode == "per_record" else 1))
+    ad_stride = ad_len if ad_mode == "per_record" else 0
+    pt = rng.randbytes(length * nrec)
+    d_out = torch.zeros((length + 16) * nrec, dtype=torch.uint8, device="cuda")
+    noise_amd.encrypt_uniform(key, n0, dev(pt), length, d_out, length + 16, length, nrec,
+                              d_ad=dev(ad), ad_stride=ad_stride, ad_len=ad_len)
+    out = host(d_out)
+    for i in range(nrec):
+        a = ad[i * ad_stride:i * ad_stride + ad_len]
+        assert out[i * (length + 16):(i + 1) * (length + 16)] == \
+            oracle.encrypt(key, n0 + i, a, pt[i * length:(i + 1) * length])
+
+
+@pytest.mark.parametrize("n0", [2**32 - 3, 2**64 - 3, 2**64 - 1, 2**63 - 2])
+def test_nonce_edges(oracle, n0):
+    """Nonce words 14/15 carry, and (nonce0 + i) wrapping mod 2^64."""
+    rng = random.Random(n0 & 0xffff)
+    key, nrec, length = rng.randbytes(32), 8, 64
+    pt = rng.randbytes(length * nrec)
+    d_out = torch.zeros((length + 16) * nrec, dtype=torch.uint8, device="cuda")
+    noise_amd.encrypt_uniform(key, n0, dev(pt), length, d_out, length + 16, length, nrec)
+    out = host(d_out)
+    for i in range(nrec):
+        assert out[i * 80:(i + 1) * 80] == oracle.encrypt(key, (n0 + i) % 2**64, b"",
+                                                           pt[i * 64:(i + 1) * 64])
+
+
+@pytest.mark.parametrize("in_place", [False, True])
+@pytest.mark.parametrize("length", [1024, 77])
+def test_decrypt_rejects_tampering(oracle, in_place, length):
+    rng = random.Random(length + in_place)
+    nrec = 64
+    stride = (length + 16 + 15) & ~15
+    key, n0 = rng.randbytes(32), rng.getrandbits(40)
+    buf = bytearray(stride * nrec)
+    for i in range(nrec):
+        buf[i * stride:i * stride + length + 16] = oracle.encrypt(key, n0 + i, b"",
+                                                                  rng.randbytes(length))
+    orig = bytes(buf)
+    bad = {3: 0, 17: length + 5, 40: length + 15, 63: length // 2}  # record -> byte flipped
+    for i, off in bad.items():
+        buf[i * stride + off] ^= 0x01
+    tampered = bytes(buf)
+    d_in = dev(tampered)
+    d_out = d_in if in_place else torch.full((stride * nrec,), 0xAB, dtype=torch.uint8, device="cuda")
+    d_st = torch.full((nrec,), 9, dtype=torch.uint8, device="cuda")
+    noise_amd.decrypt_uniform(key, n0, d_in, stride, d_out, stride, length, d_st, nrec)
+    st = host(d_st)
+    out = host(d_out)
+    for i in range(nrec):
+        rec = out[i * stride:i * stride + length]
+        if i in bad:
+            assert st[i] == noise_amd.REC_BAD_MAC
+            # in place: buffer untouched; out of place: no unauthenticated plaintext
+            want = tampered[i * stride:i * stride + length] if in_place else bytes(length)
+            assert rec == want, i
+        else:
+            assert st[i] == noise_amd.REC_OK
+            assert rec == oracle.decrypt(key, n0 + i, b"", orig[i * stride:i * stride + length + 16])
+
+
+def test_in_place_encrypt(oracle):
+    rng = random.Random(5)
+    nrec, length, stride = 100, 512, 528
+    key = rng.randbytes(32)
+    buf = bytearray(stride * nrec)
+    pts = [rng.randbytes(length) for _ in range(nrec)]
+    for i, p in enumerate(pts):
+        buf[i * stride:i * stride + length] = p
+    d = dev(bytes(buf))
+    noise_amd.encrypt_uniform(key, 0, d, stride, d, stride, length, nrec)
+    out = host(d)
+    for i, p in enumerate(pts):
+        assert out[i * stride:(i + 1) * stride] == oracle.encrypt(key, i, b"", p)
+
+
+def test_many_sessions_records(oracle):
+    """Config-3 shape at reduced size: 4096 keys x 4 records, interleaved,
+    nonce = (s << 32) + j (exercises nonce word 15)."""
+    rng = random.Random(9)
+    nkeys, per, length = 4096, 4, 1024
+    keys = [rng.randbytes(32) for _ in range(nkeys)]
+    nrec = nkeys * per
+    pt = np.frombuffer(rng.randbytes(nrec * length), dtype=np.uint8)
+    desc = np.zeros(nrec, dtype=noise_amd.record_dtype())
+    i = np.arange(nrec, dtype=np.uint64)
+    desc["in_off"] = i * length
+    desc["out_off"] = i * (length + 16)
+    s = i % nkeys
+    desc["nonce"] = (s << np.uint64(32)) + i // nkeys
+    desc["len"] = length
+    desc["key_idx"] = s.astype(np.uint32)
+    d_out = torch.zeros(nrec * (length + 16), dtype=torch.uint8, device="cuda")
+    d_keys = dev(b"".join(keys))
+    noise_amd.encrypt_records(d_keys, nkeys, dev(desc.view(np.uint8)), nrec, dev(pt), d_out)
+    out = host(d_out)
+    for j in rng.sample(range(nrec), 300) + [0, nrec - 1]:
+        want = oracle.encrypt(keys[j % nkeys], int(desc["nonce"][j]), b"",
+                              pt[j * length:(j + 1) * length].tobytes())
+        assert out[j * (length + 16):(j + 1) * (length + 16)] == want, j
+
+
+def test_fill_synthetic_matches_oracle(oracle):
+    for offset, n in [(0, 4096), (16, 1000), (3, 77)]:
+        d = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        noise_amd.fill_synthetic(d, n, SEED, offset=offset)
+        assert host(d) == oracle.synthetic(n, SEED, offset=offset)
+
+
+def test_config2_full_size_round_trip(oracle):
+    """BASELINE config 2 at full size: 2^20 x 1 KiB, one key, nonces 0..R-1.
+    Size-independent properties: every tag verifies, decrypt(encrypt(x)) == x,
+    and a random sample (plus the first/last records) equals the oracle."""
+    R, L = 1 << 20, 1024
+    key = bytes(range(32))
+    d_pt = torch.empty(R * L, dtype=torch.uint8, device="cuda")
+    noise_amd.fill_synthetic(d_pt, R * L, SEED)
+    d_ct = torch.empty(R * (L + 16), dtype=torch.uint8, device="cuda")
+    d_back = torch.empty(R * L, dtype=torch.uint8, device="cuda")
+    d_st = torch.full((R,), 9, dtype=torch.uint8, device="cuda")
+    noise_amd.encrypt_uniform(key, 0, d_pt, L, d_ct, L + 16, L, R)
+    noise_amd.decrypt_uniform(key, 0, d_ct, L + 16, d_back, L, L, d_st, R)
+    torch.cuda.synchronize()
+    assert int(d_st.sum().item()) == 0
+    assert torch.equal(d_pt, d_back)
+    ct = d_ct.view(R, L + 16)
+    rng = random.Random(2)
+    for i in rng.sample(range(R), 256) + [0, R - 1]:
+        p = oracle.synthetic(L, SEED, offset=i * L)
+        assert ct[i].cpu().numpy().tobytes() == oracle.encrypt(key, i, b"", p), i
+
+
+def test_host_pipeline_matches_device(oracle):
+    """Transfer-inclusive host API == device kernels (pinned buffers)."""
+    rng = random.Random(4)
+    R, L = 3000, 1024
+    key = rng.randbytes(32)
+    pt = torch.from_numpy(np.frombuffer(rng.randbytes(R * L), dtype=np.uint8).copy()).pin_memory()
+    ct = torch.zeros(R * (L + 16), dtype=torch.uint8).pin_memory()
+    back = torch.zeros(R * L, dtype=torch.uint8).pin_memory()
+    st = torch.full((R,), 9, dtype=torch.uint8).pin_memory()
+    import ctypes
+    lib = noise_amd.load()
+    secs = ctypes.c_double()
+    assert lib.noise_gpu_encrypt_uniform_host(key, 10, ctypes.c_void_p(pt.data_ptr()), L,
+                                              ctypes.c_void_p(ct.data_ptr()), L + 16, L, R,
+                                              ctypes.byref(secs)) == 0
+    assert lib.noise_gpu_decrypt_uniform_host(key, 10, ctypes.c_void_p(ct.data_ptr()), L + 16,
+                                              ctypes.c_void_p(back.data_ptr()), L, L,
+                                              ctypes.c_void_p(st.data_ptr()), R,
+                                              ctypes.byref(secs)) == 0
+    assert torch.equal(pt, back) and int(st.sum()) == 0
+    c = ct.numpy().tobytes()
+    for i in (0, 1, 1234, R - 1):
+        assert c[i * (L + 16):(i + 1) * (L + 16)] == oracle.encrypt(
+            key, 10 + i, b"", pt[i * L:(i + 1) * L].numpy().tobytes())
+
+
+def test_cipherstate_cpp_surface():
+    """The drop-in noise::CipherState (C++20) on the golden records."""
+    exe = os.path.join(noise_amd.ROOT, "noise-cpp_amd", "bin", "cipherstate_test")
+    r = subprocess.run([exe, os.path.join(noise_amd.ROOT, "tests", "golden")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "PASSED" in r.stdout

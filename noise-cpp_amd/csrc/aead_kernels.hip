@@ -13,14 +13,11 @@
 // workgroups, one record per thread; the grid covers nrec.
 #include "chachapoly_device.hpp"
 #include "launchers.hpp"
+#include "tile_kernel.hpp"
 
 namespace noise_amd {
 
 constexpr int kBlock = 256;
-
-struct KeyArg {
-  uint32_t w[8];
-};
 
 template <bool DECRYPT, bool VEC>
 __global__ __launch_bounds__(kBlock) void k_aead_uniform(
@@ -125,6 +122,30 @@ hipError_t launch_aead_uniform(bool decrypt, const uint32_t key[8],
   const bool vec = ((reinterpret_cast<uintptr_t>(in) |
                      reinterpret_cast<uintptr_t>(out) | in_stride |
                      out_stride | len) & 15u) == 0;
+  // LDS-staged tile kernel: aligned, AD-free, supported lengths
+  if (vec && ad_len == 0) {
+    const int in_place = in == out;
+    const dim3 gt((unsigned)((nrec + 63) / 64)), bt(64);
+#define NOISE_TILE_CASE(LEN)                                                   \
+    case LEN:                                                                  \
+      if (decrypt)                                                             \
+        hipLaunchKernelGGL((k_aead_tile<true, LEN>), gt, bt, 0, stream, k, nonce0, in, in_stride, out, out_stride, status, nrec, in_place); \
+      else                                                                     \
+        hipLaunchKernelGGL((k_aead_tile<false, LEN>), gt, bt, 0, stream, k, nonce0, in, in_stride, out, out_stride, status, nrec, in_place); \
+      return hipGetLastError();
+    switch (len) {
+      NOISE_TILE_CASE(64)
+      NOISE_TILE_CASE(128)
+      NOISE_TILE_CASE(192)
+      NOISE_TILE_CASE(256)
+      NOISE_TILE_CASE(512)
+      NOISE_TILE_CASE(1024)
+      NOISE_TILE_CASE(2048)
+      NOISE_TILE_CASE(4096)
+      default: break;
+    }
+#undef NOISE_TILE_CASE
+  }
   const dim3 g = grid_for(nrec), b(kBlock);
   if (decrypt) {
     if (vec)

@@ -23,6 +23,11 @@
 
 namespace noise_amd {
 
+// A 32-byte key passed by value as a kernel argument (lands in SGPRs).
+struct KeyArg {
+  uint32_t w[8];
+};
+
 // "expand 32-byte k"
 constexpr uint32_t kSigma0 = 0x61707865u, kSigma1 = 0x3320646eu,
                    kSigma2 = 0x79622d32u, kSigma3 = 0x6b206574u;
@@ -149,6 +154,76 @@ __device__ __forceinline__ void poly_final(const Poly1305 &p, uint32_t tag[4]) {
   tag[2] = (uint32_t)c;
   c = (c >> 32) + (uint64_t)p.h3 + p.s3;
   tag[3] = (uint32_t)c;
+}
+
+// ------------------------------------------------ general Poly1305 products
+// Radix-2^26 arithmetic for multiplying by an arbitrary element (powers of
+// r are not "clamped", so the radix-2^32 shortcut above does not apply).
+// Used only to recombine a record's per-lane partial Horner sums
+// (O(log G) products per lane per record), never in the per-block loop.
+constexpr uint32_t kM26 = 0x3ffffffu;
+
+struct F26 {
+  uint32_t a[5];
+};
+
+__device__ __forceinline__ F26 to26(uint32_t h0, uint32_t h1, uint32_t h2,
+                                    uint32_t h3, uint32_t h4) {
+  F26 f;
+  f.a[0] = h0 & kM26;
+  f.a[1] = __builtin_amdgcn_alignbit(h1, h0, 26) & kM26;
+  f.a[2] = __builtin_amdgcn_alignbit(h2, h1, 20) & kM26;
+  f.a[3] = __builtin_amdgcn_alignbit(h3, h2, 14) & kM26;
+  f.a[4] = (h3 >> 8) | (h4 << 24);
+  return f;
+}
+
+// value (any limb sizes < 2^31) -> radix 2^32 words h0..h3 and small h4
+__device__ __forceinline__ void from26(const F26 &f, uint32_t &h0, uint32_t &h1,
+                                       uint32_t &h2, uint32_t &h3, uint32_t &h4) {
+  uint64_t w = (uint64_t)f.a[0] + ((uint64_t)f.a[1] << 26);
+  h0 = (uint32_t)w;
+  w = (w >> 32) + ((uint64_t)f.a[2] << 20);
+  h1 = (uint32_t)w;
+  w = (w >> 32) + ((uint64_t)f.a[3] << 14);
+  h2 = (uint32_t)w;
+  w = (w >> 32) + ((uint64_t)f.a[4] << 8);
+  h3 = (uint32_t)w;
+  h4 = (uint32_t)(w >> 32);
+}
+
+// full carry propagation modulo 2^130-5 (limbs < 2^31 in, < 2^26(+1) out)
+__device__ __forceinline__ void carry26(F26 &f) {
+  uint32_t c;
+  c = f.a[0] >> 26; f.a[0] &= kM26; f.a[1] += c;
+  c = f.a[1] >> 26; f.a[1] &= kM26; f.a[2] += c;
+  c = f.a[2] >> 26; f.a[2] &= kM26; f.a[3] += c;
+  c = f.a[3] >> 26; f.a[3] &= kM26; f.a[4] += c;
+  c = f.a[4] >> 26; f.a[4] &= kM26; f.a[0] += c * 5u;
+  c = f.a[0] >> 26; f.a[0] &= kM26; f.a[1] += c;
+}
+
+// x * y mod 2^130-5; x limbs < 2^27, y limbs < 2^26 (+1)
+__device__ __forceinline__ F26 mul26(const F26 &x, const F26 &y) {
+  const uint32_t y1 = y.a[1] * 5u, y2 = y.a[2] * 5u, y3 = y.a[3] * 5u,
+                 y4 = y.a[4] * 5u;
+  const uint32_t *a = x.a, *b = y.a;
+  uint64_t d0 = mad64(a[0], b[0], mad64(a[1], y4, mad64(a[2], y3, mad64(a[3], y2, mad64(a[4], y1, 0)))));
+  uint64_t d1 = mad64(a[0], b[1], mad64(a[1], b[0], mad64(a[2], y4, mad64(a[3], y3, mad64(a[4], y2, 0)))));
+  uint64_t d2 = mad64(a[0], b[2], mad64(a[1], b[1], mad64(a[2], b[0], mad64(a[3], y4, mad64(a[4], y3, 0)))));
+  uint64_t d3 = mad64(a[0], b[3], mad64(a[1], b[2], mad64(a[2], b[1], mad64(a[3], b[0], mad64(a[4], y4, 0)))));
+  uint64_t d4 = mad64(a[0], b[4], mad64(a[1], b[3], mad64(a[2], b[2], mad64(a[3], b[1], mad64(a[4], b[0], 0)))));
+  F26 r;
+  uint32_t c;
+  c = (uint32_t)(d0 >> 26); r.a[0] = (uint32_t)d0 & kM26; d1 += c;
+  c = (uint32_t)(d1 >> 26); r.a[1] = (uint32_t)d1 & kM26; d2 += c;
+  c = (uint32_t)(d2 >> 26); r.a[2] = (uint32_t)d2 & kM26; d3 += c;
+  c = (uint32_t)(d3 >> 26); r.a[3] = (uint32_t)d3 & kM26; d4 += c;
+  c = (uint32_t)(d4 >> 26); r.a[4] = (uint32_t)d4 & kM26;
+  const uint64_t t = (uint64_t)c * 5u + r.a[0];  // c < 2^32, so widen
+  r.a[0] = (uint32_t)t & kM26;
+  r.a[1] += (uint32_t)(t >> 26);
+  return r;
 }
 
 // ---------------------------------------------------------------- memory

@@ -1,0 +1,221 @@
+// tile_kernel.hpp -- the LDS-staged ("tile") AEAD kernel for uniform-length,
+// 16-byte aligned, AD-free record batches (the transport hot path).
+//
+// Why: the lane-per-record walk reads/writes each record in 16-byte pieces
+// spread over 64 records per wave-instruction; on MI355X that access shape
+// runs at ~0.5 TB/s.  Whole-record, lane-contiguous wave-instructions (1 KiB
+// each) run at copy speed.  So records move HBM <-> LDS in whole-record,
+// coalesced wave-instructions (LDS-DMA `global_load_lds_dwordx4` in,
+// `ds_read_b128` + `global_store_dwordx4` out) and the arithmetic reads its
+// pieces from LDS.
+//
+// Work split (one 64-thread workgroup = one wave = one "super-tile" of 64
+// consecutive records):
+//   * key pass: lane l computes ChaCha block 0 of record l (r, s) and, for
+//     G > 1, the Poly1305 powers r^16, r^32, ... it will hand out;
+//   * G = max(1, L/256) lanes per record, RPT = 64/G records per tile,
+//     G tiles per super-tile.  Lane j of a record owns the contiguous
+//     256-byte span [256j, 256j+256): 4 ChaCha blocks (counters 1+4j..4+4j)
+//     and 16 Poly1305 blocks, Horner-evaluated with the clamped r;
+//   * the G partial sums recombine as  sum_j acc_j * r^(16(G-1-j)),
+//     log2(G) general products per lane + a log2(G)-step butterfly.
+// LDS image per tile: RPT*L/16 16-byte slots (plaintext/ciphertext, XOR-
+// swizzled within 16-slot groups so the per-lane ds_read/ds_write_b128 are
+// bank-conflict free) + RPT tag slots.  The swizzle is applied on the
+// global SOURCE address of the LDS-DMA (its LDS destination is lane-linear).
+#pragma once
+#include "chachapoly_device.hpp"
+
+namespace noise_amd {
+
+template <int L>
+struct TileCfg {
+  static constexpr int G = L >= 256 ? L / 256 : 1;  // lanes per record
+  static constexpr int RPT = 64 / G;                // records per tile
+  static constexpr int CPL = (L / 64) / G;          // 64-B chunks per lane
+  static constexpr int SPR = L / 16;                // 16-B slots per record
+  static constexpr int REC_SLOTS = RPT * SPR;
+  static constexpr int NSLOT = REC_SLOTS + RPT;     // + one tag slot per record
+  static constexpr int LOG2G = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : 4;
+  static_assert(L % 64 == 0 && 64 % G == 0 && (L < 256 || L % 256 == 0), "tile shape");
+};
+
+template <int L>
+constexpr bool tile_supported() {
+  return L == 64 || L == 128 || L == 192 || L == 256 || L == 512 ||
+         L == 1024 || L == 2048 || L == 4096;
+}
+
+// slot <-> piece involution inside each aligned 16-slot group
+__device__ __forceinline__ uint32_t swz(uint32_t s) { return s ^ ((s >> 4) & 15u); }
+
+template <bool DECRYPT, int L>
+__global__ __launch_bounds__(64) void k_aead_tile(
+    KeyArg key, uint64_t nonce0, const uint8_t *in, uint64_t in_stride,
+    uint8_t *out, uint64_t out_stride, uint8_t *status, uint64_t nrec,
+    int in_place) {
+  using C = TileCfg<L>;
+  __shared__ uint4 lds[C::NSLOT];
+  const uint32_t lane = threadIdx.x;
+  const uint64_t super0 = (uint64_t)blockIdx.x * 64;
+  uint32_t k[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) k[i] = key.w[i];
+
+  // ---- key pass: lane l -> one-time key of record super0 + l -------------
+  uint32_t kr[4], kss[4];
+  F26 pw[C::LOG2G > 0 ? C::LOG2G : 1];
+  {
+    const uint64_t n = nonce0 + super0 + lane;
+    uint32_t otk[16];
+    chacha20_block(k, 0u, (uint32_t)n, (uint32_t)(n >> 32), otk);
+    kr[0] = otk[0] & 0x0fffffffu;
+    kr[1] = otk[1] & 0x0ffffffcu;
+    kr[2] = otk[2] & 0x0ffffffcu;
+    kr[3] = otk[3] & 0x0ffffffcu;
+    kss[0] = otk[4]; kss[1] = otk[5]; kss[2] = otk[6]; kss[3] = otk[7];
+    if (C::G > 1) {
+      const F26 r1 = to26(kr[0], kr[1], kr[2], kr[3], 0u);
+      F26 x = mul26(r1, r1);  // r^2
+      x = mul26(x, x);        // r^4
+      x = mul26(x, x);        // r^8
+      x = mul26(x, x);        // r^16
+      pw[0] = x;
+#pragma unroll
+      for (int b = 1; b < C::LOG2G; ++b) pw[b] = mul26(pw[b - 1], pw[b - 1]);
+    }
+  }
+
+  const uint32_t rho = lane / C::G, j = lane % C::G;
+#pragma unroll 1
+  for (int t = 0; t < C::G; ++t) {
+    const uint64_t rec0 = super0 + (uint64_t)t * C::RPT;
+    if (rec0 >= nrec) break;
+    const uint32_t nv = (nrec - rec0) < (uint64_t)C::RPT ? (uint32_t)(nrec - rec0) : C::RPT;
+
+    // ---- HBM -> LDS, whole records per wave-instruction ------------------
+    constexpr int IN_SLOTS = DECRYPT ? C::NSLOT : C::REC_SLOTS;
+#pragma unroll 1
+    for (int q = 0; q < (IN_SLOTS + 63) / 64; ++q) {
+      const uint32_t s = 64u * q + lane;
+      uint32_t r, p;
+      if (s < (uint32_t)C::REC_SLOTS) {
+        const uint32_t g = swz(s);
+        r = g / C::SPR;
+        p = g % C::SPR;
+      } else {  // decrypt: tag slots
+        r = s - C::REC_SLOTS;
+        p = C::SPR;
+      }
+      if (s < (uint32_t)IN_SLOTS && r < nv)
+        __builtin_amdgcn_global_load_lds(
+            (const void *)(in + (rec0 + r) * in_stride + 16u * p),
+            (__attribute__((address_space(3))) void *)(lds + 64 * q), 16, 0, 0);
+    }
+    __syncthreads();  // the compiler drains the LDS-DMA (vmcnt) before it
+
+    // ---- per-lane record work -------------------------------------------
+    const uint32_t src = (uint32_t)t * C::RPT + rho;  // key lane of my record
+    uint32_t r4[4], s4[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      r4[i] = __shfl(kr[i], src);
+      s4[i] = __shfl(kss[i], src);
+    }
+    Poly1305 p;
+    p.r0 = r4[0]; p.r1 = r4[1]; p.r2 = r4[2]; p.r3 = r4[3];
+    p.rr0 = (p.r0 >> 2) * 5u;
+    p.rr1 = p.r1 + (p.r1 >> 2);
+    p.rr2 = p.r2 + (p.r2 >> 2);
+    p.rr3 = p.r3 + (p.r3 >> 2);
+    p.r0lo = p.r0 & 3u;
+    p.s0 = s4[0]; p.s1 = s4[1]; p.s2 = s4[2]; p.s3 = s4[3];
+    p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0;
+
+    const uint64_t n = nonce0 + rec0 + rho;
+    const uint32_t n_lo = (uint32_t)n, n_hi = (uint32_t)(n >> 32);
+#pragma unroll 1
+    for (int kk = 0; kk < C::CPL; ++kk) {
+      const uint32_t c = j * C::CPL + kk;
+      uint32_t ks[16];
+      chacha20_block(k, 1u + c, n_lo, n_hi, ks);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t slot = swz(rho * C::SPR + 4u * c + q);
+        const uint4 v = lds[slot];
+        uint4 o;
+        o.x = v.x ^ ks[4 * q + 0];
+        o.y = v.y ^ ks[4 * q + 1];
+        o.z = v.z ^ ks[4 * q + 2];
+        o.w = v.w ^ ks[4 * q + 3];
+        lds[slot] = o;
+        if (DECRYPT) poly_block(p, v.x, v.y, v.z, v.w);
+        else poly_block(p, o.x, o.y, o.z, o.w);
+      }
+    }
+    if (C::G > 1) {
+      // acc_j * r^(16 (G-1-j)), then sum over the record's G lanes
+      F26 h = to26(p.h0, p.h1, p.h2, p.h3, p.h4);
+      const uint32_t m = C::G - 1 - j;
+#pragma unroll
+      for (int b = 0; b < C::LOG2G; ++b) {
+        F26 f;
+        const bool use = (m >> b) & 1u;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+          const uint32_t w = __shfl(pw[b].a[i], src);
+          f.a[i] = use ? w : (i == 0 ? 1u : 0u);
+        }
+        h = mul26(h, f);
+      }
+#pragma unroll
+      for (int b = 0; b < C::LOG2G; ++b) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) h.a[i] += __shfl_xor(h.a[i], 1 << b);
+      }
+      carry26(h);
+      carry26(h);
+      from26(h, p.h0, p.h1, p.h2, p.h3, p.h4);
+    }
+    poly_block(p, 0u, 0u, (uint32_t)L, 0u);  // LE64(ad_len = 0) || LE64(L)
+    uint32_t tag[4];
+    poly_final(p, tag);
+    const bool valid = rho < nv;
+    if (DECRYPT) {
+      const uint4 want = lds[C::REC_SLOTS + rho];
+      const uint32_t diff = (want.x ^ tag[0]) | (want.y ^ tag[1]) |
+                            (want.z ^ tag[2]) | (want.w ^ tag[3]);
+      __syncthreads();  // every lane has read its tag slot
+      if (j == 0) {
+        lds[C::REC_SLOTS + rho].x = diff ? 1u : 0u;  // reuse as fail flag
+        if (valid) status[rec0 + rho] = diff ? 1u : 0u;
+      }
+    } else if (j == 0) {
+      lds[C::REC_SLOTS + rho] = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+    }
+    __syncthreads();
+
+    // ---- LDS -> HBM, whole output records per wave-instruction -----------
+    constexpr int OPR = DECRYPT ? C::SPR : C::SPR + 1;  // out pieces / record
+    constexpr int OUT_SLOTS = C::RPT * OPR;
+#pragma unroll 1
+    for (int q = 0; q < (OUT_SLOTS + 63) / 64; ++q) {
+      const uint32_t g = 64u * q + lane;
+      const uint32_t r = g / OPR, pc = g % OPR;
+      if (g < (uint32_t)OUT_SLOTS && r < nv) {
+        const uint32_t slot = pc < (uint32_t)C::SPR ? swz(r * C::SPR + pc) : C::REC_SLOTS + r;
+        uint4 v = lds[slot];
+        bool store = true;
+        if (DECRYPT && lds[C::REC_SLOTS + r].x != 0u) {
+          // failed tag: leave an in-place record untouched, zero a copy
+          store = !in_place;
+          v = make_uint4(0u, 0u, 0u, 0u);
+        }
+        if (store) store16<true>(out + (rec0 + r) * out_stride + 16u * pc, v, 16);
+      }
+    }
+    __syncthreads();  // LDS reads done before the next tile's DMA lands
+  }
+}
+
+}  // namespace noise_amd

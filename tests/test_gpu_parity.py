@@ -113,8 +113,43 @@ def test_kats_and_rekey(oracle):
     assert all(got[32 * i:32 * i + 32] == oracle.rekey(k) for i, k in enumerate(keys))
 
 
-LENGTHS = [0, 1, 3, 15, 16, 17, 31, 32, 48, 63, 64, 65, 100, 127, 128, 129, 255, 256, 1000,
-           1023, 1024, 1025, 1040, 4096, 65519]
+LENGTHS = [0, 1, 3, 15, 16, 17, 31, 32, 48, 63, 64, 65, 100, 127, 128, 129, 192, 255, 256, 512,
+           1000, 1023, 1024, 1025, 1040, 2048, 4096, 65519]
+
+# lengths served by the LDS-staged tile kernel (tile_kernel.hpp)
+TILE_LENGTHS = [64, 128, 192, 256, 512, 1024, 2048, 4096]
+
+
+@pytest.mark.parametrize("length", TILE_LENGTHS)
+@pytest.mark.parametrize("nrec", [1, 63, 64, 65, 200, 1000])
+@pytest.mark.parametrize("in_place", [False, True])
+def test_tile_kernel_shapes(oracle, length, nrec, in_place):
+    """Partial tiles / super-tiles, in-place and out-of-place, both directions."""
+    rng = random.Random(length * 1000 + nrec * 2 + in_place)
+    key, n0 = rng.randbytes(32), rng.getrandbits(64)
+    in_stride = length + 16 if in_place else length
+    out_stride = length + 16 if in_place else length + 32  # padded output rows
+    pts = [rng.randbytes(length) for _ in range(nrec)]
+    src = bytearray(in_stride * nrec)
+    for i, p in enumerate(pts):
+        src[i * in_stride:i * in_stride + length] = p
+    d_in = dev(bytes(src))
+    d_out = d_in if in_place else torch.zeros(out_stride * nrec, dtype=torch.uint8, device="cuda")
+    noise_amd.encrypt_uniform(key, n0, d_in, in_stride, d_out, out_stride, length, nrec)
+    out = host(d_out)
+    for i in list(range(min(nrec, 70))) + list(range(max(0, nrec - 70), nrec)):
+        want = oracle.encrypt(key, n0 + i, b"", pts[i])
+        assert out[i * out_stride:i * out_stride + length + 16] == want, i
+    # decrypt (into separate rows, or back in place)
+    d_pt = d_out if in_place else torch.zeros(in_stride * nrec, dtype=torch.uint8, device="cuda")
+    d_st = torch.full((nrec,), 9, dtype=torch.uint8, device="cuda")
+    noise_amd.decrypt_uniform(key, n0, d_out, out_stride, d_pt, out_stride if in_place else in_stride,
+                              length, d_st, nrec)
+    assert set(host(d_st)) == {0}
+    back = host(d_pt)
+    st = out_stride if in_place else in_stride
+    for i in range(nrec):
+        assert back[i * st:i * st + length] == pts[i], i
 
 
 @pytest.mark.parametrize("length", LENGTHS)

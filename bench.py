@@ -45,6 +45,24 @@ def shard(total, rank, world):
     return total * rank // world, total * (rank + 1) // world
 
 
+def rank_nonce_base(cfg, rank, world, per_rank, total):
+    """First nonce of a rank's records: weak scaling (cfg 2) gives every rank
+    its own R-record nonce range; strong scaling (cfg 5) splits one range."""
+    if cfg == 2:
+        return rank * per_rank
+    return shard(total, rank, world)[0]
+
+
+def reduce_over_ranks(dist, elapsed, nrec, device):
+    """Max of the elapsed time and sum of the records over ranks."""
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    n = torch.tensor([nrec], dtype=torch.int64, device=device)
+    dist.all_reduce(n)
+    return float(t.item()), int(n.item())
+
+
 def pmc_traffic(workload):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if any
     (profiles/*/pmc_traffic.json, written from a separate --pmc pass)."""
@@ -119,7 +137,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--min-warmup-s", type=float, default=0.3,
+                    help="keep running untimed warmup steps until this much wall time has passed "
+                         "(the GPU clock ramps over ~0.1 s; see DESIGN.md)")
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
     ap.add_argument("--records", type=int, default=0, help="override records per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -145,12 +166,12 @@ def main():
         workload = "cfg2: 2^20 x 1 KiB records per GPU, one key, encrypt+decrypt round trip"
         if args.records:
             workload = "cfg2-shape: %d x 1 KiB records per GPU" % R
-        n_base = rank * R
+        n_base = rank_nonce_base(cfg, rank, world, R, R * world)
     elif cfg == 5:  # strong scaling: 8 Mi x 4 KiB split over the GPUs
         total = args.records or (8 << 20)
         lo, hi = shard(total, rank, world)
         R, L = hi - lo, 4096
-        n_base = lo
+        n_base = rank_nonce_base(cfg, rank, world, R, total)
         workload = "cfg5: %d x 4 KiB records total, sharded over %d GPU(s)" % (total, world)
     else:
         raise SystemExit("configs 3/4 are parity-test shapes; bench line uses 2 (or 5)")
@@ -174,9 +195,13 @@ def main():
             evs[2].record(stream)
 
     log("rank %d/%d: %d records x %d B, warmup %d" % (rank, world, R, L, args.warmup))
+    tw = time.perf_counter()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    while time.perf_counter() - tw < args.min_warmup_s:
+        step()
+        torch.cuda.synchronize()
     # correctness of what is about to be timed: all tags verify, round trip exact
     ok = int(d_st.sum().item()) == 0 and torch.equal(d_pt, d_back)
     if not ok:
@@ -194,12 +219,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        nrec_all = torch.tensor([R], dtype=torch.int64, device="cuda")
-        dist.all_reduce(nrec_all)
-        total_rec = int(nrec_all.item())
+        elapsed, total_rec = reduce_over_ranks(dist, elapsed, R, "cuda")
     else:
         total_rec = R
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps

@@ -126,12 +126,20 @@ hipError_t launch_aead_uniform(bool decrypt, const uint32_t key[8],
   if (vec && ad_len == 0) {
     const int in_place = in == out;
     const dim3 gt((unsigned)((nrec + 63) / 64)), bt(64);
+    // packed records (stride == record size on both sides): cheap addressing
+    const bool contig = decrypt ? (in_stride == (uint64_t)len + 16 && out_stride == len)
+                                : (in_stride == len && out_stride == (uint64_t)len + 16);
+#define NOISE_TILE_LAUNCH(DEC, LEN, CONTIG)                                    \
+    hipLaunchKernelGGL((k_aead_tile<DEC, LEN, CONTIG>), gt, bt, 0, stream, k, nonce0, in, in_stride, out, out_stride, status, nrec, in_place)
 #define NOISE_TILE_CASE(LEN)                                                   \
     case LEN:                                                                  \
-      if (decrypt)                                                             \
-        hipLaunchKernelGGL((k_aead_tile<true, LEN>), gt, bt, 0, stream, k, nonce0, in, in_stride, out, out_stride, status, nrec, in_place); \
-      else                                                                     \
-        hipLaunchKernelGGL((k_aead_tile<false, LEN>), gt, bt, 0, stream, k, nonce0, in, in_stride, out, out_stride, status, nrec, in_place); \
+      if (decrypt) {                                                           \
+        if (contig) NOISE_TILE_LAUNCH(true, LEN, true);                        \
+        else NOISE_TILE_LAUNCH(true, LEN, false);                              \
+      } else {                                                                 \
+        if (contig) NOISE_TILE_LAUNCH(false, LEN, true);                       \
+        else NOISE_TILE_LAUNCH(false, LEN, false);                             \
+      }                                                                        \
       return hipGetLastError();
     switch (len) {
       NOISE_TILE_CASE(64)
@@ -145,6 +153,7 @@ hipError_t launch_aead_uniform(bool decrypt, const uint32_t key[8],
       default: break;
     }
 #undef NOISE_TILE_CASE
+#undef NOISE_TILE_LAUNCH
   }
   const dim3 g = grid_for(nrec), b(kBlock);
   if (decrypt) {

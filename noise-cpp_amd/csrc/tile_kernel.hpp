@@ -49,7 +49,9 @@ constexpr bool tile_supported() {
 // slot <-> piece involution inside each aligned 16-slot group
 __device__ __forceinline__ uint32_t swz(uint32_t s) { return s ^ ((s >> 4) & 15u); }
 
-template <bool DECRYPT, int L>
+// ABL (ablation, tools/ubench only; the product uses 0): 1 = no HBM traffic
+// (compute on whatever the LDS holds), 2 = no Poly1305 work.
+template <bool DECRYPT, int L, bool CONTIG, int ABL = 0>
 __global__ __launch_bounds__(64) void k_aead_tile(
     KeyArg key, uint64_t nonce0, const uint8_t *in, uint64_t in_stride,
     uint8_t *out, uint64_t out_stride, uint8_t *status, uint64_t nrec,
@@ -87,6 +89,10 @@ __global__ __launch_bounds__(64) void k_aead_tile(
   }
 
   const uint32_t rho = lane / C::G, j = lane % C::G;
+  // swz(64q + lane) - 64q depends on q only through q & 3
+  uint32_t gl[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) gl[i] = swz(64u * i + lane) - 64u * i;
 #pragma unroll 1
   for (int t = 0; t < C::G; ++t) {
     const uint64_t rec0 = super0 + (uint64_t)t * C::RPT;
@@ -95,22 +101,49 @@ __global__ __launch_bounds__(64) void k_aead_tile(
 
     // ---- HBM -> LDS, whole records per wave-instruction ------------------
     constexpr int IN_SLOTS = DECRYPT ? C::NSLOT : C::REC_SLOTS;
-#pragma unroll 1
-    for (int q = 0; q < (IN_SLOTS + 63) / 64; ++q) {
-      const uint32_t s = 64u * q + lane;
-      uint32_t r, p;
-      if (s < (uint32_t)C::REC_SLOTS) {
-        const uint32_t g = swz(s);
-        r = g / C::SPR;
-        p = g % C::SPR;
-      } else {  // decrypt: tag slots
-        r = s - C::REC_SLOTS;
-        p = C::SPR;
+    if (CONTIG) {
+      // slot s = 64q + lane holds piece swz(s) = 64q + gl[q & 3]; packed
+      // records put piece g of an encrypt tile at byte 16g and of a decrypt
+      // tile (65-piece records) at 16(g + g/64).
+      const uint8_t *base = in + rec0 * in_stride;
+#pragma unroll
+      for (int q = 0; q < C::REC_SLOTS / 64; ++q) {
+        const uint32_t g = 64u * q + gl[q & 3];
+        const uint32_t rr = g / C::SPR;
+        const uint32_t off = DECRYPT ? 16u * (g + rr) : 16u * g;
+        if (ABL != 1 && rr < nv)
+          __builtin_amdgcn_global_load_lds(
+              (const void *)(base + off),
+              (__attribute__((address_space(3))) void *)(lds + 64 * q), 16, 0, 0);
       }
-      if (s < (uint32_t)IN_SLOTS && r < nv)
-        __builtin_amdgcn_global_load_lds(
-            (const void *)(in + (rec0 + r) * in_stride + 16u * p),
-            (__attribute__((address_space(3))) void *)(lds + 64 * q), 16, 0, 0);
+      if (DECRYPT) {  // tag pieces: slot REC_SLOTS + r <- piece (r, SPR)
+#pragma unroll
+        for (int q = C::REC_SLOTS / 64; q < (C::NSLOT + 63) / 64; ++q) {
+          const uint32_t r = 64u * q + lane - C::REC_SLOTS;
+          if (ABL != 1 && r < nv)
+            __builtin_amdgcn_global_load_lds(
+                (const void *)(base + 16u * (r * (C::SPR + 1) + C::SPR)),
+                (__attribute__((address_space(3))) void *)(lds + 64 * q), 16, 0, 0);
+        }
+      }
+    } else {
+#pragma unroll 1
+      for (int q = 0; q < (IN_SLOTS + 63) / 64; ++q) {
+        const uint32_t s = 64u * q + lane;
+        uint32_t r, p;
+        if (s < (uint32_t)C::REC_SLOTS) {
+          const uint32_t g = swz(s);
+          r = g / C::SPR;
+          p = g % C::SPR;
+        } else {  // decrypt: tag slots
+          r = s - C::REC_SLOTS;
+          p = C::SPR;
+        }
+        if (ABL != 1 && s < (uint32_t)IN_SLOTS && r < nv)
+          __builtin_amdgcn_global_load_lds(
+              (const void *)(in + (rec0 + r) * in_stride + 16u * p),
+              (__attribute__((address_space(3))) void *)(lds + 64 * q), 16, 0, 0);
+      }
     }
     __syncthreads();  // the compiler drains the LDS-DMA (vmcnt) before it
 
@@ -134,11 +167,18 @@ __global__ __launch_bounds__(64) void k_aead_tile(
 
     const uint64_t n = nonce0 + rec0 + rho;
     const uint32_t n_lo = (uint32_t)n, n_hi = (uint32_t)(n >> 32);
-#pragma unroll 1
+    // Software pipeline: the ChaCha block of chunk kk+1 is independent of
+    // the (serial) Poly1305 chain of chunk kk, so both sit in one basic
+    // block and the scheduler interleaves them (ILP at ~2 waves/SIMD).
+    const uint32_t c0 = j * C::CPL;
+    const ChaPre pre = chacha_pre(k, n_lo, n_hi);
+    uint32_t ks[16];
+    chacha20_block_pre(k, 1u + c0, pre, n_lo, n_hi, ks);
+#pragma unroll
     for (int kk = 0; kk < C::CPL; ++kk) {
-      const uint32_t c = j * C::CPL + kk;
-      uint32_t ks[16];
-      chacha20_block(k, 1u + c, n_lo, n_hi, ks);
+      const uint32_t c = c0 + kk;
+      uint32_t ksn[16];
+      if (kk + 1 < C::CPL) chacha20_block_pre(k, 2u + c, pre, n_lo, n_hi, ksn);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint32_t slot = swz(rho * C::SPR + 4u * c + q);
@@ -149,8 +189,13 @@ __global__ __launch_bounds__(64) void k_aead_tile(
         o.z = v.z ^ ks[4 * q + 2];
         o.w = v.w ^ ks[4 * q + 3];
         lds[slot] = o;
-        if (DECRYPT) poly_block(p, v.x, v.y, v.z, v.w);
+        if (ABL == 2) { p.h0 ^= o.x ^ v.y; p.h1 ^= o.z ^ v.w; }
+        else if (DECRYPT) poly_block(p, v.x, v.y, v.z, v.w);
         else poly_block(p, o.x, o.y, o.z, o.w);
+      }
+      if (kk + 1 < C::CPL) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) ks[i] = ksn[i];
       }
     }
     if (C::G > 1) {
@@ -198,20 +243,42 @@ __global__ __launch_bounds__(64) void k_aead_tile(
     // ---- LDS -> HBM, whole output records per wave-instruction -----------
     constexpr int OPR = DECRYPT ? C::SPR : C::SPR + 1;  // out pieces / record
     constexpr int OUT_SLOTS = C::RPT * OPR;
-#pragma unroll 1
-    for (int q = 0; q < (OUT_SLOTS + 63) / 64; ++q) {
-      const uint32_t g = 64u * q + lane;
-      const uint32_t r = g / OPR, pc = g % OPR;
-      if (g < (uint32_t)OUT_SLOTS && r < nv) {
-        const uint32_t slot = pc < (uint32_t)C::SPR ? swz(r * C::SPR + pc) : C::REC_SLOTS + r;
-        uint4 v = lds[slot];
-        bool store = true;
-        if (DECRYPT && lds[C::REC_SLOTS + r].x != 0u) {
-          // failed tag: leave an in-place record untouched, zero a copy
-          store = !in_place;
-          v = make_uint4(0u, 0u, 0u, 0u);
+    if (CONTIG) {
+      uint8_t *base = out + rec0 * out_stride;
+#pragma unroll
+      for (int q = 0; q < (OUT_SLOTS + 63) / 64; ++q) {
+        const uint32_t g = 64u * q + lane;  // output piece, packed layout
+        const uint32_t r = g / OPR, pc = g % OPR;
+        uint32_t slot;
+        if (DECRYPT) slot = 64u * q + gl[q & 3];  // == swz(g)
+        else slot = pc < (uint32_t)C::SPR ? swz(r * C::SPR + pc) : C::REC_SLOTS + r;
+        if (g < (uint32_t)OUT_SLOTS && r < nv) {
+          uint4 v = lds[slot];
+          bool store = true;
+          if (DECRYPT && lds[C::REC_SLOTS + r].x != 0u) {
+            store = !in_place;  // failed tag: keep in-place record, zero a copy
+            v = make_uint4(0u, 0u, 0u, 0u);
+          }
+          if (ABL == 1) store = (v.x == 0x12345678u && v.y == 0x9abcdef0u);
+          if (store) store16<true>(base + 16u * g, v, 16);
         }
-        if (store) store16<true>(out + (rec0 + r) * out_stride + 16u * pc, v, 16);
+      }
+    } else {
+#pragma unroll 1
+      for (int q = 0; q < (OUT_SLOTS + 63) / 64; ++q) {
+        const uint32_t g = 64u * q + lane;
+        const uint32_t r = g / OPR, pc = g % OPR;
+        if (g < (uint32_t)OUT_SLOTS && r < nv) {
+          const uint32_t slot = pc < (uint32_t)C::SPR ? swz(r * C::SPR + pc) : C::REC_SLOTS + r;
+          uint4 v = lds[slot];
+          bool store = true;
+          if (DECRYPT && lds[C::REC_SLOTS + r].x != 0u) {
+            store = !in_place;
+            v = make_uint4(0u, 0u, 0u, 0u);
+          }
+          if (ABL == 1) store = (v.x == 0x12345678u && v.y == 0x9abcdef0u);
+          if (store) store16<true>(out + (rec0 + r) * out_stride + 16u * pc, v, 16);
+        }
       }
     }
     __syncthreads();  // LDS reads done before the next tile's DMA lands

@@ -195,19 +195,24 @@ def main():
             evs[2].record(stream)
 
     log("rank %d/%d: %d records x %d B, warmup %d" % (rank, world, R, L, args.warmup))
+    # correctness of the step about to be timed: all tags verify, round trip
+    # exact (checked before the warmup so no host-side idle gap -- during which
+    # the GPU clock drops -- separates the warmup from the timed steps)
+    step()
+    torch.cuda.synchronize()
+    ok = int(d_st.sum().item()) == 0 and torch.equal(d_pt, d_back)
+    if not ok:
+        raise SystemExit("round trip failed on rank %d" % rank)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     tw = time.perf_counter()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     while time.perf_counter() - tw < args.min_warmup_s:
-        step()
+        for _ in range(4):
+            step()
         torch.cuda.synchronize()
-    # correctness of what is about to be timed: all tags verify, round trip exact
-    ok = int(d_st.sum().item()) == 0 and torch.equal(d_pt, d_back)
-    if not ok:
-        raise SystemExit("round trip failed on rank %d" % rank)
 
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -222,6 +227,9 @@ def main():
         elapsed, total_rec = reduce_over_ranks(dist, elapsed, R, "cuda")
     else:
         total_rec = R
+    # the timed work was correct too
+    if int(d_st.sum().item()) != 0 or not torch.equal(d_pt, d_back):
+        raise SystemExit("timed round trip failed on rank %d" % rank)
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
     log("enc %.3f ms, dec %.3f ms per launch; step %.3f ms" %

@@ -19,6 +19,12 @@
 //     and 16 Poly1305 blocks, Horner-evaluated with the clamped r;
 //   * the G partial sums recombine as  sum_j acc_j * r^(16(G-1-j)),
 //     log2(G) general products per lane + a log2(G)-step butterfly.
+// Per tile the wave does: compute (LDS in place) -> gather the output
+// records into VGPRs -> issue the NEXT tile's LDS-DMA and THIS tile's global
+// stores back to back, so the two memory round trips overlap; the only
+// memory wait is the one before the next compute.  A workgroup is a single
+// wave, so no s_barrier is needed: LDS ordering is program order within the
+// wave (the fences below only stop the compiler from moving LDS accesses).
 // LDS image per tile: RPT*L/16 16-byte slots (plaintext/ciphertext, XOR-
 // swizzled within 16-slot groups so the per-lane ds_read/ds_write_b128 are
 // bank-conflict free) + RPT tag slots.  The swizzle is applied on the
@@ -40,14 +46,68 @@ struct TileCfg {
   static_assert(L % 64 == 0 && 64 % G == 0 && (L < 256 || L % 256 == 0), "tile shape");
 };
 
-template <int L>
-constexpr bool tile_supported() {
-  return L == 64 || L == 128 || L == 192 || L == 256 || L == 512 ||
-         L == 1024 || L == 2048 || L == 4096;
-}
-
 // slot <-> piece involution inside each aligned 16-slot group
 __device__ __forceinline__ uint32_t swz(uint32_t s) { return s ^ ((s >> 4) & 15u); }
+
+// compiler-level LDS ordering point for a single-wave workgroup
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int L, bool DECRYPT, bool CONTIG, int ABL>
+__device__ __forceinline__ void tile_load(uint4 *lds, const uint8_t *in,
+                                          uint64_t in_stride, uint64_t rec0,
+                                          uint32_t nv, uint32_t lane,
+                                          const uint32_t gl[4]) {
+  using C = TileCfg<L>;
+  if (ABL == 1) return;
+  constexpr int IN_SLOTS = DECRYPT ? C::NSLOT : C::REC_SLOTS;
+  if (CONTIG) {
+    // slot s = 64q + lane holds piece swz(s) = 64q + gl[q & 3]; packed
+    // records put piece g of an encrypt tile at byte 16g and of a decrypt
+    // tile (SPR+1 pieces per record) at 16(g + g/SPR).
+    const uint8_t *base = in + rec0 * in_stride;
+#pragma unroll
+    for (int q = 0; q < C::REC_SLOTS / 64; ++q) {
+      const uint32_t g = 64u * q + gl[q & 3];
+      const uint32_t rr = g / C::SPR;
+      const uint32_t off = DECRYPT ? 16u * (g + rr) : 16u * g;
+      if (rr < nv)
+        __builtin_amdgcn_global_load_lds(
+            (const void *)(base + off),
+            (__attribute__((address_space(3))) void *)(lds + 64 * q), 16, 0, 0);
+    }
+    if (DECRYPT) {  // tag pieces: slot REC_SLOTS + r <- piece (r, SPR)
+#pragma unroll
+      for (int q = C::REC_SLOTS / 64; q < (C::NSLOT + 63) / 64; ++q) {
+        const uint32_t r = 64u * q + lane - C::REC_SLOTS;
+        if (r < nv)
+          __builtin_amdgcn_global_load_lds(
+              (const void *)(base + 16u * (r * (C::SPR + 1) + C::SPR)),
+              (__attribute__((address_space(3))) void *)(lds + 64 * q), 16, 0, 0);
+      }
+    }
+  } else {
+#pragma unroll 1
+    for (int q = 0; q < (IN_SLOTS + 63) / 64; ++q) {
+      const uint32_t s = 64u * q + lane;
+      uint32_t r, p;
+      if (s < (uint32_t)C::REC_SLOTS) {
+        const uint32_t g = swz(s);
+        r = g / C::SPR;
+        p = g % C::SPR;
+      } else {  // decrypt: tag slots
+        r = s - C::REC_SLOTS;
+        p = C::SPR;
+      }
+      if (s < (uint32_t)IN_SLOTS && r < nv)
+        __builtin_amdgcn_global_load_lds(
+            (const void *)(in + (rec0 + r) * in_stride + 16u * p),
+            (__attribute__((address_space(3))) void *)(lds + 64 * q), 16, 0, 0);
+    }
+  }
+}
 
 // ABL (ablation, tools/ubench only; the product uses 0): 1 = no HBM traffic
 // (compute on whatever the LDS holds), 2 = no Poly1305 work.
@@ -57,12 +117,29 @@ __global__ __launch_bounds__(64) void k_aead_tile(
     uint8_t *out, uint64_t out_stride, uint8_t *status, uint64_t nrec,
     int in_place) {
   using C = TileCfg<L>;
+  constexpr int OPR = DECRYPT ? C::SPR : C::SPR + 1;  // out pieces / record
+  constexpr int OUT_SLOTS = C::RPT * OPR;
+  constexpr int NOUT = (OUT_SLOTS + 63) / 64;          // store instructions
   __shared__ uint4 lds[C::NSLOT];
   const uint32_t lane = threadIdx.x;
   const uint64_t super0 = (uint64_t)blockIdx.x * 64;
   uint32_t k[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) k[i] = key.w[i];
+
+  const uint32_t rho = lane / C::G, j = lane % C::G;
+  // swz(64q + lane) - 64q depends on q only through q & 3
+  uint32_t gl[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) gl[i] = swz(64u * i + lane) - 64u * i;
+
+  // the first tile's DMA goes out before the key pass and lands meanwhile
+  {
+    const uint64_t left = nrec - super0;
+    tile_load<L, DECRYPT, CONTIG, ABL>(lds, in, in_stride, super0,
+                                       left < (uint64_t)C::RPT ? (uint32_t)left : C::RPT,
+                                       lane, gl);
+  }
 
   // ---- key pass: lane l -> one-time key of record super0 + l -------------
   uint32_t kr[4], kss[4];
@@ -88,88 +165,35 @@ __global__ __launch_bounds__(64) void k_aead_tile(
     }
   }
 
-  const uint32_t rho = lane / C::G, j = lane % C::G;
-  // swz(64q + lane) - 64q depends on q only through q & 3
-  uint32_t gl[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) gl[i] = swz(64u * i + lane) - 64u * i;
 #pragma unroll 1
   for (int t = 0; t < C::G; ++t) {
     const uint64_t rec0 = super0 + (uint64_t)t * C::RPT;
     if (rec0 >= nrec) break;
     const uint32_t nv = (nrec - rec0) < (uint64_t)C::RPT ? (uint32_t)(nrec - rec0) : C::RPT;
 
-    // ---- HBM -> LDS, whole records per wave-instruction ------------------
-    constexpr int IN_SLOTS = DECRYPT ? C::NSLOT : C::REC_SLOTS;
-    if (CONTIG) {
-      // slot s = 64q + lane holds piece swz(s) = 64q + gl[q & 3]; packed
-      // records put piece g of an encrypt tile at byte 16g and of a decrypt
-      // tile (65-piece records) at 16(g + g/64).
-      const uint8_t *base = in + rec0 * in_stride;
-#pragma unroll
-      for (int q = 0; q < C::REC_SLOTS / 64; ++q) {
-        const uint32_t g = 64u * q + gl[q & 3];
-        const uint32_t rr = g / C::SPR;
-        const uint32_t off = DECRYPT ? 16u * (g + rr) : 16u * g;
-        if (ABL != 1 && rr < nv)
-          __builtin_amdgcn_global_load_lds(
-              (const void *)(base + off),
-              (__attribute__((address_space(3))) void *)(lds + 64 * q), 16, 0, 0);
-      }
-      if (DECRYPT) {  // tag pieces: slot REC_SLOTS + r <- piece (r, SPR)
-#pragma unroll
-        for (int q = C::REC_SLOTS / 64; q < (C::NSLOT + 63) / 64; ++q) {
-          const uint32_t r = 64u * q + lane - C::REC_SLOTS;
-          if (ABL != 1 && r < nv)
-            __builtin_amdgcn_global_load_lds(
-                (const void *)(base + 16u * (r * (C::SPR + 1) + C::SPR)),
-                (__attribute__((address_space(3))) void *)(lds + 64 * q), 16, 0, 0);
-        }
-      }
-    } else {
-#pragma unroll 1
-      for (int q = 0; q < (IN_SLOTS + 63) / 64; ++q) {
-        const uint32_t s = 64u * q + lane;
-        uint32_t r, p;
-        if (s < (uint32_t)C::REC_SLOTS) {
-          const uint32_t g = swz(s);
-          r = g / C::SPR;
-          p = g % C::SPR;
-        } else {  // decrypt: tag slots
-          r = s - C::REC_SLOTS;
-          p = C::SPR;
-        }
-        if (ABL != 1 && s < (uint32_t)IN_SLOTS && r < nv)
-          __builtin_amdgcn_global_load_lds(
-              (const void *)(in + (rec0 + r) * in_stride + 16u * p),
-              (__attribute__((address_space(3))) void *)(lds + 64 * q), 16, 0, 0);
-      }
-    }
-    __syncthreads();  // the compiler drains the LDS-DMA (vmcnt) before it
+    // this tile's DMA (and the previous tile's stores) must have landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_lds_fence();
 
     // ---- per-lane record work -------------------------------------------
     const uint32_t src = (uint32_t)t * C::RPT + rho;  // key lane of my record
-    uint32_t r4[4], s4[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      r4[i] = __shfl(kr[i], src);
-      s4[i] = __shfl(kss[i], src);
-    }
     Poly1305 p;
-    p.r0 = r4[0]; p.r1 = r4[1]; p.r2 = r4[2]; p.r3 = r4[3];
+    p.r0 = __shfl(kr[0], src); p.r1 = __shfl(kr[1], src);
+    p.r2 = __shfl(kr[2], src); p.r3 = __shfl(kr[3], src);
     p.rr0 = (p.r0 >> 2) * 5u;
     p.rr1 = p.r1 + (p.r1 >> 2);
     p.rr2 = p.r2 + (p.r2 >> 2);
     p.rr3 = p.r3 + (p.r3 >> 2);
     p.r0lo = p.r0 & 3u;
-    p.s0 = s4[0]; p.s1 = s4[1]; p.s2 = s4[2]; p.s3 = s4[3];
+    p.s0 = __shfl(kss[0], src); p.s1 = __shfl(kss[1], src);
+    p.s2 = __shfl(kss[2], src); p.s3 = __shfl(kss[3], src);
     p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0;
 
     const uint64_t n = nonce0 + rec0 + rho;
     const uint32_t n_lo = (uint32_t)n, n_hi = (uint32_t)(n >> 32);
     // Software pipeline: the ChaCha block of chunk kk+1 is independent of
     // the (serial) Poly1305 chain of chunk kk, so both sit in one basic
-    // block and the scheduler interleaves them (ILP at ~2 waves/SIMD).
+    // block and the scheduler interleaves them.
     const uint32_t c0 = j * C::CPL;
     const ChaPre pre = chacha_pre(k, n_lo, n_hi);
     uint32_t ks[16];
@@ -226,62 +250,60 @@ __global__ __launch_bounds__(64) void k_aead_tile(
     uint32_t tag[4];
     poly_final(p, tag);
     const bool valid = rho < nv;
+    uint64_t fail_mask = 0;  // bit (r * G): record r of this tile failed its tag
     if (DECRYPT) {
       const uint4 want = lds[C::REC_SLOTS + rho];
       const uint32_t diff = (want.x ^ tag[0]) | (want.y ^ tag[1]) |
                             (want.z ^ tag[2]) | (want.w ^ tag[3]);
-      __syncthreads();  // every lane has read its tag slot
-      if (j == 0) {
-        lds[C::REC_SLOTS + rho].x = diff ? 1u : 0u;  // reuse as fail flag
-        if (valid) status[rec0 + rho] = diff ? 1u : 0u;
-      }
+      fail_mask = __ballot(j == 0 && diff != 0u);
+      if (j == 0 && valid) status[rec0 + rho] = diff ? 1u : 0u;
     } else if (j == 0) {
       lds[C::REC_SLOTS + rho] = make_uint4(tag[0], tag[1], tag[2], tag[3]);
     }
-    __syncthreads();
+    wave_lds_fence();
 
-    // ---- LDS -> HBM, whole output records per wave-instruction -----------
-    constexpr int OPR = DECRYPT ? C::SPR : C::SPR + 1;  // out pieces / record
-    constexpr int OUT_SLOTS = C::RPT * OPR;
-    if (CONTIG) {
-      uint8_t *base = out + rec0 * out_stride;
+    // ---- gather this tile's output records into registers ----------------
+    uint4 ov[NOUT];
+    bool st[NOUT];
+    const bool full = nv == (uint32_t)C::RPT;
 #pragma unroll
-      for (int q = 0; q < (OUT_SLOTS + 63) / 64; ++q) {
-        const uint32_t g = 64u * q + lane;  // output piece, packed layout
-        const uint32_t r = g / OPR, pc = g % OPR;
-        uint32_t slot;
-        if (DECRYPT) slot = 64u * q + gl[q & 3];  // == swz(g)
-        else slot = pc < (uint32_t)C::SPR ? swz(r * C::SPR + pc) : C::REC_SLOTS + r;
-        if (g < (uint32_t)OUT_SLOTS && r < nv) {
-          uint4 v = lds[slot];
-          bool store = true;
-          if (DECRYPT && lds[C::REC_SLOTS + r].x != 0u) {
-            store = !in_place;  // failed tag: keep in-place record, zero a copy
-            v = make_uint4(0u, 0u, 0u, 0u);
-          }
-          if (ABL == 1) store = (v.x == 0x12345678u && v.y == 0x9abcdef0u);
-          if (store) store16<true>(base + 16u * g, v, 16);
-        }
-      }
-    } else {
-#pragma unroll 1
-      for (int q = 0; q < (OUT_SLOTS + 63) / 64; ++q) {
-        const uint32_t g = 64u * q + lane;
-        const uint32_t r = g / OPR, pc = g % OPR;
-        if (g < (uint32_t)OUT_SLOTS && r < nv) {
-          const uint32_t slot = pc < (uint32_t)C::SPR ? swz(r * C::SPR + pc) : C::REC_SLOTS + r;
-          uint4 v = lds[slot];
-          bool store = true;
-          if (DECRYPT && lds[C::REC_SLOTS + r].x != 0u) {
-            store = !in_place;
-            v = make_uint4(0u, 0u, 0u, 0u);
-          }
-          if (ABL == 1) store = (v.x == 0x12345678u && v.y == 0x9abcdef0u);
-          if (store) store16<true>(out + (rec0 + r) * out_stride + 16u * pc, v, 16);
-        }
+    for (int q = 0; q < NOUT; ++q) {
+      const uint32_t g = 64u * q + lane;  // output piece (record r, piece pc)
+      const uint32_t r = g / OPR, pc = g % OPR;
+      uint32_t slot;
+      if (CONTIG && DECRYPT) slot = 64u * q + gl[q & 3];  // == swz(g)
+      else slot = pc < (uint32_t)C::SPR ? swz(r * C::SPR + pc) : C::REC_SLOTS + r;
+      st[q] = (OUT_SLOTS % 64 == 0 || g < (uint32_t)OUT_SLOTS) && (full || r < nv);
+      ov[q] = lds[slot < (uint32_t)C::NSLOT ? slot : 0u];
+      if (DECRYPT && fail_mask != 0 && ((fail_mask >> (r * C::G)) & 1u)) {
+        st[q] = st[q] && !in_place;  // failed tag: keep in-place record, zero a copy
+        ov[q] = make_uint4(0u, 0u, 0u, 0u);
       }
     }
-    __syncthreads();  // LDS reads done before the next tile's DMA lands
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS reads done
+    wave_lds_fence();
+
+    // ---- next tile's DMA, then this tile's stores: both in flight at once
+    if (t + 1 < C::G) {
+      const uint64_t nrec0 = rec0 + C::RPT;
+      if (nrec0 < nrec) {
+        const uint64_t left = nrec - nrec0;
+        tile_load<L, DECRYPT, CONTIG, ABL>(lds, in, in_stride, nrec0,
+                                           left < (uint64_t)C::RPT ? (uint32_t)left : C::RPT,
+                                           lane, gl);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NOUT; ++q) {
+      const uint32_t g = 64u * q + lane;
+      const uint32_t r = g / OPR, pc = g % OPR;
+      bool store = st[q];
+      if (ABL == 1) store = store && (ov[q].x == 0x12345678u && ov[q].y == 0x9abcdef0u);
+      if (store) {
+        const uint64_t off = CONTIG ? 16ull * g : r * out_stride + 16u * pc;
+        store16<true>(out + rec0 * out_stride + off, ov[q], 16);
+      }
+    }
   }
 }
 

@@ -115,6 +115,30 @@ int noise_gpu_decrypt_records(const uint8_t *d_keys, uint32_t nkeys,
                               const uint8_t *d_ad, uint8_t *d_status,
                               void *stream);
 
+/* ---- device-resident many-session batches (BASELINE config 3) ---------
+ * nrec records of `len` plaintext bytes, record i under key row
+ * d_keys[d_key_idx[i]] (a [nkeys][32] table, 16-byte aligned) with Noise
+ * nonce d_nonces[i]; records laid out like the uniform batches (d_in + i *
+ * in_stride, d_out + i * out_stride).  No associated data (transport).
+ * Served by the LDS-staged tile kernel: len in {64, 128, 192, 256, 512,
+ * 1024, 2048, 4096} with 16-byte aligned buffers/strides; other shapes
+ * return NOISE_GPU_E_ARG (use the descriptor functions below).  A record
+ * whose key index is >= nkeys is not written; decrypt marks it
+ * NOISE_GPU_REC_BAD_KEY. */
+#define NOISE_GPU_REC_BAD_KEY 2u
+int noise_gpu_encrypt_sessions(const uint8_t *d_keys, uint32_t nkeys,
+                               const uint32_t *d_key_idx,
+                               const uint64_t *d_nonces, const uint8_t *d_in,
+                               uint64_t in_stride, uint8_t *d_out,
+                               uint64_t out_stride, uint32_t len, uint64_t nrec,
+                               void *stream);
+int noise_gpu_decrypt_sessions(const uint8_t *d_keys, uint32_t nkeys,
+                               const uint32_t *d_key_idx,
+                               const uint64_t *d_nonces, const uint8_t *d_in,
+                               uint64_t in_stride, uint8_t *d_out,
+                               uint64_t out_stride, uint32_t len,
+                               uint8_t *d_status, uint64_t nrec, void *stream);
+
 /* REKEY of every key in a device key table, in place:
  * k <- ENCRYPT(k, 2^64-2, empty, 0^32)[0..32)   (noise.cpp:429-439). */
 int noise_gpu_rekey_keys(uint8_t *d_keys, uint64_t nkeys, void *stream);

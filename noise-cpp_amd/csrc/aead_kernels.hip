@@ -130,7 +130,7 @@ hipError_t launch_aead_uniform(bool decrypt, const uint32_t key[8],
     const bool contig = decrypt ? (in_stride == (uint64_t)len + 16 && out_stride == len)
                                 : (in_stride == len && out_stride == (uint64_t)len + 16);
 #define NOISE_TILE_LAUNCH(DEC, LEN, CONTIG)                                    \
-    hipLaunchKernelGGL((k_aead_tile<DEC, LEN, CONTIG>), gt, bt, 0, stream, k, nonce0, in, in_stride, out, out_stride, status, nrec, in_place)
+    hipLaunchKernelGGL((k_aead_tile<DEC, LEN, CONTIG>), gt, bt, 0, stream, k, nonce0, in, in_stride, out, out_stride, status, nrec, in_place, nullptr, nullptr, nullptr, 0u)
 #define NOISE_TILE_CASE(LEN)                                                   \
     case LEN:                                                                  \
       if (decrypt) {                                                           \

@@ -76,20 +76,22 @@ __device__ __forceinline__ void chacha20_block(const uint32_t k[8],
   ks[14] = x14 + n_lo;   ks[15] = x15 + n_hi;
 }
 
-// Round-1 columns 2 and 3 depend only on (key, nonce), not on the block
+// Round-1 columns 1, 2 and 3 depend only on (key, nonce), not on the block
 // counter, so a lane that runs several blocks of one record computes them
 // once (chacha_pre) and starts each block from them (chacha20_block_pre):
-// 2 of the 80 quarter-rounds per block saved.  Column 1 (x13 = 0) is
-// uniform across the wave for a single key and runs on the scalar unit.
+// 3 of the 80 quarter-rounds per block saved (column 1 -- x13 = 0 -- is
+// wave-uniform for a single key and then runs on the scalar unit anyway).
 struct ChaPre {
-  uint32_t x2, x6, x10, x14, x3, x7, x11, x15;
+  uint32_t x1, x5, x9, x13, x2, x6, x10, x14, x3, x7, x11, x15;
 };
 
 __device__ __forceinline__ ChaPre chacha_pre(const uint32_t k[8], uint32_t n_lo,
                                              uint32_t n_hi) {
   ChaPre p;
+  p.x1 = kSigma1; p.x5 = k[1]; p.x9 = k[5]; p.x13 = 0u;
   p.x2 = kSigma2; p.x6 = k[2]; p.x10 = k[6]; p.x14 = n_lo;
   p.x3 = kSigma3; p.x7 = k[3]; p.x11 = k[7]; p.x15 = n_hi;
+  NOISE_QR(p.x1, p.x5, p.x9, p.x13)
   NOISE_QR(p.x2, p.x6, p.x10, p.x14)
   NOISE_QR(p.x3, p.x7, p.x11, p.x15)
   return p;
@@ -100,13 +102,12 @@ __device__ __forceinline__ void chacha20_block_pre(const uint32_t k[8],
                                                    const ChaPre &pre,
                                                    uint32_t n_lo, uint32_t n_hi,
                                                    uint32_t ks[16]) {
-  uint32_t x0 = kSigma0, x1 = kSigma1, x2 = pre.x2, x3 = pre.x3;
-  uint32_t x4 = k[0], x5 = k[1], x6 = pre.x6, x7 = pre.x7;
-  uint32_t x8 = k[4], x9 = k[5], x10 = pre.x10, x11 = pre.x11;
-  uint32_t x12 = ctr, x13 = 0, x14 = pre.x14, x15 = pre.x15;
-  // round 1: columns 0 and 1 (2 and 3 come precomputed), then diagonals
+  uint32_t x0 = kSigma0, x1 = pre.x1, x2 = pre.x2, x3 = pre.x3;
+  uint32_t x4 = k[0], x5 = pre.x5, x6 = pre.x6, x7 = pre.x7;
+  uint32_t x8 = k[4], x9 = pre.x9, x10 = pre.x10, x11 = pre.x11;
+  uint32_t x12 = ctr, x13 = pre.x13, x14 = pre.x14, x15 = pre.x15;
+  // round 1: column 0 (the only counter-dependent one), then diagonals
   NOISE_QR(x0, x4, x8, x12)
-  NOISE_QR(x1, x5, x9, x13)
   NOISE_QR(x0, x5, x10, x15)
   NOISE_QR(x1, x6, x11, x12)
   NOISE_QR(x2, x7, x8, x13)

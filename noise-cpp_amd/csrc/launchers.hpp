@@ -22,6 +22,17 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
                                const uint8_t *ad, uint8_t *status,
                                hipStream_t stream);
 
+bool sessions_supported(uint32_t len, const void *in, uint64_t in_stride,
+                        const void *out, uint64_t out_stride);
+
+hipError_t launch_aead_sessions(bool decrypt, const uint8_t *keys,
+                                uint32_t nkeys, const uint32_t *key_idx,
+                                const uint64_t *nonces, const uint8_t *in,
+                                uint64_t in_stride, uint8_t *out,
+                                uint64_t out_stride, uint32_t len,
+                                uint8_t *status, uint64_t nrec,
+                                hipStream_t stream);
+
 hipError_t launch_rekey(uint8_t *keys, uint64_t nkeys, hipStream_t stream);
 
 hipError_t launch_fill_synthetic(uint8_t *dst, uint64_t offset,

@@ -218,6 +218,50 @@ int noise_gpu_decrypt_records(const uint8_t *d_keys, uint32_t nkeys,
   return NOISE_GPU_OK;
 }
 
+static int sessions(bool decrypt, const uint8_t *d_keys, uint32_t nkeys,
+                    const uint32_t *d_key_idx, const uint64_t *d_nonces,
+                    const uint8_t *d_in, uint64_t in_stride, uint8_t *d_out,
+                    uint64_t out_stride, uint32_t len, uint8_t *d_status,
+                    uint64_t nrec, void *stream) {
+  if (nrec == 0) return NOISE_GPU_OK;
+  if (!d_keys || !nkeys || !d_key_idx || !d_nonces)
+    return arg_fail("null key table / key index / nonce array");
+  if (reinterpret_cast<uintptr_t>(d_keys) & 15u)
+    return arg_fail("key table must be 16-byte aligned");
+  int rc = check_uniform(decrypt, d_in, in_stride, d_out, out_stride, len,
+                         nullptr, 0, d_status, nrec);
+  if (rc) return rc;
+  if (!noise_amd::sessions_supported(len, d_in, in_stride, d_out, out_stride))
+    return arg_fail("sessions batches need len in {64,128,192,256,512,1024,2048,4096} "
+                    "and 16-byte aligned buffers/strides");
+  if ((rc = check_device())) return rc;
+  HIP_TRY(noise_amd::launch_aead_sessions(decrypt, d_keys, nkeys, d_key_idx,
+                                          d_nonces, d_in, in_stride, d_out,
+                                          out_stride, len, d_status, nrec,
+                                          (hipStream_t)stream));
+  return NOISE_GPU_OK;
+}
+
+int noise_gpu_encrypt_sessions(const uint8_t *d_keys, uint32_t nkeys,
+                               const uint32_t *d_key_idx,
+                               const uint64_t *d_nonces, const uint8_t *d_in,
+                               uint64_t in_stride, uint8_t *d_out,
+                               uint64_t out_stride, uint32_t len, uint64_t nrec,
+                               void *stream) {
+  return sessions(false, d_keys, nkeys, d_key_idx, d_nonces, d_in, in_stride,
+                  d_out, out_stride, len, nullptr, nrec, stream);
+}
+
+int noise_gpu_decrypt_sessions(const uint8_t *d_keys, uint32_t nkeys,
+                               const uint32_t *d_key_idx,
+                               const uint64_t *d_nonces, const uint8_t *d_in,
+                               uint64_t in_stride, uint8_t *d_out,
+                               uint64_t out_stride, uint32_t len,
+                               uint8_t *d_status, uint64_t nrec, void *stream) {
+  return sessions(true, d_keys, nkeys, d_key_idx, d_nonces, d_in, in_stride,
+                  d_out, out_stride, len, d_status, nrec, stream);
+}
+
 int noise_gpu_rekey_keys(uint8_t *d_keys, uint64_t nkeys, void *stream) {
   if (nkeys == 0) return NOISE_GPU_OK;
   if (!d_keys) return arg_fail("null key table");

@@ -109,13 +109,18 @@ __device__ __forceinline__ void tile_load(uint4 *lds, const uint8_t *in,
   }
 }
 
+// KEYED = true ("sessions" batch): record i uses key row
+// s_keys[s_key_idx[i]] and nonce s_nonces[i]; a key index outside the table
+// makes the record fail (nothing written; decrypt status 2).
 // ABL (ablation, tools/ubench only; the product uses 0): 1 = no HBM traffic
 // (compute on whatever the LDS holds), 2 = no Poly1305 work.
-template <bool DECRYPT, int L, bool CONTIG, int ABL = 0>
+template <bool DECRYPT, int L, bool CONTIG, bool KEYED = false, int ABL = 0>
 __global__ __launch_bounds__(64) void k_aead_tile(
     KeyArg key, uint64_t nonce0, const uint8_t *in, uint64_t in_stride,
     uint8_t *out, uint64_t out_stride, uint8_t *status, uint64_t nrec,
-    int in_place) {
+    int in_place, const uint8_t *__restrict__ s_keys,
+    const uint32_t *__restrict__ s_key_idx, const uint64_t *__restrict__ s_nonces,
+    uint32_t s_nkeys) {
   using C = TileCfg<L>;
   constexpr int OPR = DECRYPT ? C::SPR : C::SPR + 1;  // out pieces / record
   constexpr int OUT_SLOTS = C::RPT * OPR;
@@ -144,10 +149,32 @@ __global__ __launch_bounds__(64) void k_aead_tile(
   // ---- key pass: lane l -> one-time key of record super0 + l -------------
   uint32_t kr[4], kss[4];
   F26 pw[C::LOG2G > 0 ? C::LOG2G : 1];
+  uint32_t own_k[8], own_nlo = 0, own_nhi = 0;  // KEYED: this lane's record
+  bool own_bad = false;
   {
-    const uint64_t n = nonce0 + super0 + lane;
+    uint64_t n = nonce0 + super0 + lane;
+    if (KEYED) {
+      const uint64_t rec = super0 + lane;
+      uint32_t ki = 0;
+      n = 0;
+      if (rec < nrec) {
+        ki = __builtin_nontemporal_load(s_key_idx + rec);
+        n = __builtin_nontemporal_load(s_nonces + rec);
+      }
+      own_bad = ki >= s_nkeys;
+      if (own_bad) ki = 0;
+      const u32x4 *kp = reinterpret_cast<const u32x4 *>(s_keys + 32ull * ki);
+      const u32x4 ka = __builtin_nontemporal_load(kp), kb = __builtin_nontemporal_load(kp + 1);
+      own_k[0] = ka.x; own_k[1] = ka.y; own_k[2] = ka.z; own_k[3] = ka.w;
+      own_k[4] = kb.x; own_k[5] = kb.y; own_k[6] = kb.z; own_k[7] = kb.w;
+      own_nlo = (uint32_t)n;
+      own_nhi = (uint32_t)(n >> 32);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) own_k[i] = k[i];
+    }
     uint32_t otk[16];
-    chacha20_block(k, 0u, (uint32_t)n, (uint32_t)(n >> 32), otk);
+    chacha20_block(own_k, 0u, (uint32_t)n, (uint32_t)(n >> 32), otk);
     kr[0] = otk[0] & 0x0fffffffu;
     kr[1] = otk[1] & 0x0ffffffcu;
     kr[2] = otk[2] & 0x0ffffffcu;
@@ -189,20 +216,32 @@ __global__ __launch_bounds__(64) void k_aead_tile(
     p.s2 = __shfl(kss[2], src); p.s3 = __shfl(kss[3], src);
     p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0;
 
-    const uint64_t n = nonce0 + rec0 + rho;
-    const uint32_t n_lo = (uint32_t)n, n_hi = (uint32_t)(n >> 32);
+    uint32_t n_lo, n_hi;
+    bool bad_key = false;
+    uint32_t kt[8];  // this record's key
+#pragma unroll
+    for (int i = 0; i < 8; ++i) kt[i] = KEYED ? __shfl(own_k[i], src) : k[i];
+    if (KEYED) {
+      n_lo = __shfl(own_nlo, src);
+      n_hi = __shfl(own_nhi, src);
+      bad_key = __shfl((int)own_bad, src) != 0;
+    } else {
+      const uint64_t n = nonce0 + rec0 + rho;
+      n_lo = (uint32_t)n;
+      n_hi = (uint32_t)(n >> 32);
+    }
     // Software pipeline: the ChaCha block of chunk kk+1 is independent of
     // the (serial) Poly1305 chain of chunk kk, so both sit in one basic
     // block and the scheduler interleaves them.
     const uint32_t c0 = j * C::CPL;
-    const ChaPre pre = chacha_pre(k, n_lo, n_hi);
+    const ChaPre pre = chacha_pre(kt, n_lo, n_hi);
     uint32_t ks[16];
-    chacha20_block_pre(k, 1u + c0, pre, n_lo, n_hi, ks);
+    chacha20_block_pre(kt, 1u + c0, pre, n_lo, n_hi, ks);
 #pragma unroll
     for (int kk = 0; kk < C::CPL; ++kk) {
       const uint32_t c = c0 + kk;
       uint32_t ksn[16];
-      if (kk + 1 < C::CPL) chacha20_block_pre(k, 2u + c, pre, n_lo, n_hi, ksn);
+      if (kk + 1 < C::CPL) chacha20_block_pre(kt, 2u + c, pre, n_lo, n_hi, ksn);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint32_t slot = swz(rho * C::SPR + 4u * c + q);
@@ -250,13 +289,15 @@ __global__ __launch_bounds__(64) void k_aead_tile(
     uint32_t tag[4];
     poly_final(p, tag);
     const bool valid = rho < nv;
-    uint64_t fail_mask = 0;  // bit (r * G): record r of this tile failed its tag
+    uint64_t fail_mask = 0;  // bit (r * G): record r of this tile is not output
+    const uint64_t badk_mask = KEYED ? __ballot(j == 0 && bad_key) : 0ull;
+    fail_mask = badk_mask;
     if (DECRYPT) {
       const uint4 want = lds[C::REC_SLOTS + rho];
       const uint32_t diff = (want.x ^ tag[0]) | (want.y ^ tag[1]) |
                             (want.z ^ tag[2]) | (want.w ^ tag[3]);
-      fail_mask = __ballot(j == 0 && diff != 0u);
-      if (j == 0 && valid) status[rec0 + rho] = diff ? 1u : 0u;
+      fail_mask |= __ballot(j == 0 && diff != 0u);
+      if (j == 0 && valid) status[rec0 + rho] = bad_key ? 2u : (diff ? 1u : 0u);
     } else if (j == 0) {
       lds[C::REC_SLOTS + rho] = make_uint4(tag[0], tag[1], tag[2], tag[3]);
     }
@@ -275,8 +316,11 @@ __global__ __launch_bounds__(64) void k_aead_tile(
       else slot = pc < (uint32_t)C::SPR ? swz(r * C::SPR + pc) : C::REC_SLOTS + r;
       st[q] = (OUT_SLOTS % 64 == 0 || g < (uint32_t)OUT_SLOTS) && (full || r < nv);
       ov[q] = lds[slot < (uint32_t)C::NSLOT ? slot : 0u];
-      if (DECRYPT && fail_mask != 0 && ((fail_mask >> (r * C::G)) & 1u)) {
-        st[q] = st[q] && !in_place;  // failed tag: keep in-place record, zero a copy
+      if ((DECRYPT || KEYED) && fail_mask != 0 && ((fail_mask >> (r * C::G)) & 1u)) {
+        // failed tag (decrypt): keep an in-place record, zero a copy;
+        // invalid key index: write nothing
+        const bool bad_key_rec = KEYED && ((badk_mask >> (r * C::G)) & 1u);
+        st[q] = st[q] && DECRYPT && !in_place && !bad_key_rec;
         ov[q] = make_uint4(0u, 0u, 0u, 0u);
       }
     }

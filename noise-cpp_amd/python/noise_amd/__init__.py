@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(PKG, "lib", "libnoise_amd.so")
 HEADER = os.path.join(ROOT, "include", "noise_gpu.h")
 
 OK, E_NONCE, E_MAC, E_ARG, E_HIP, E_NODEV = 0, 1, 2, 3, 4, 5
-REC_OK, REC_BAD_MAC = 0, 1
+REC_OK, REC_BAD_MAC, REC_BAD_KEY = 0, 1, 2
 NONCE_LIMIT = (1 << 64) - 2  # noise.cpp:398 refuses n == 2^64-2
 
 
@@ -80,6 +80,10 @@ def load(path=LIB_PATH):
         "noise_gpu_encrypt_records": (ctypes.c_int, [u8p, u32, u8p, u64, u8p, u8p, u8p, vp]),
         "noise_gpu_decrypt_records": (ctypes.c_int, [u8p, u32, u8p, u64, u8p, u8p, u8p, u8p, vp]),
         "noise_gpu_rekey_keys": (ctypes.c_int, [u8p, u64, vp]),
+        "noise_gpu_encrypt_sessions": (ctypes.c_int, [u8p, u32, u8p, u8p, u8p, u64, u8p, u64, u32,
+                                                      u64, vp]),
+        "noise_gpu_decrypt_sessions": (ctypes.c_int, [u8p, u32, u8p, u8p, u8p, u64, u8p, u64, u32,
+                                                      u8p, u64, vp]),
         "noise_gpu_encrypt_host": (ctypes.c_int, [ctypes.c_char_p, u64, u8p, ctypes.c_size_t,
                                                   u8p, ctypes.c_size_t]),
         "noise_gpu_decrypt_host": (ctypes.c_int, [ctypes.c_char_p, u64, u8p, ctypes.c_size_t,
@@ -158,6 +162,22 @@ def decrypt_records(d_keys, nkeys, d_recs, nrec, d_in, d_out, d_status, d_ad=Non
     rc = load().noise_gpu_decrypt_records(_ptr(d_keys), nkeys, _ptr(d_recs), nrec, _ptr(d_in),
                                           _ptr(d_out), _ptr(d_ad), _ptr(d_status), _stream(stream))
     _check(rc, "noise_gpu_decrypt_records")
+
+
+def encrypt_sessions(d_keys, nkeys, d_key_idx, d_nonces, d_in, in_stride, d_out, out_stride,
+                     length, nrec, stream=None):
+    rc = load().noise_gpu_encrypt_sessions(_ptr(d_keys), nkeys, _ptr(d_key_idx), _ptr(d_nonces),
+                                           _ptr(d_in), in_stride, _ptr(d_out), out_stride, length,
+                                           nrec, _stream(stream))
+    _check(rc, "noise_gpu_encrypt_sessions")
+
+
+def decrypt_sessions(d_keys, nkeys, d_key_idx, d_nonces, d_in, in_stride, d_out, out_stride,
+                     length, d_status, nrec, stream=None):
+    rc = load().noise_gpu_decrypt_sessions(_ptr(d_keys), nkeys, _ptr(d_key_idx), _ptr(d_nonces),
+                                           _ptr(d_in), in_stride, _ptr(d_out), out_stride, length,
+                                           _ptr(d_status), nrec, _stream(stream))
+    _check(rc, "noise_gpu_decrypt_sessions")
 
 
 def rekey_keys(d_keys, nkeys, stream=None):

@@ -357,3 +357,76 @@ def test_cipherstate_cpp_surface():
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "PASSED" in r.stdout
+
+
+def _sessions_case(rng, nkeys, per, length):
+    keys = [rng.randbytes(32) for _ in range(nkeys)]
+    nrec = nkeys * per
+    i = np.arange(nrec, dtype=np.uint64)
+    s = (i % nkeys).astype(np.uint32)
+    nonces = (s.astype(np.uint64) << np.uint64(32)) + i // nkeys
+    pt = np.frombuffer(rng.randbytes(nrec * length), dtype=np.uint8)
+    return keys, s, nonces, pt, nrec
+
+
+@pytest.mark.parametrize("length", [64, 256, 1024, 4096])
+@pytest.mark.parametrize("packed", [True, False])
+def test_sessions_tile_kernel(oracle, length, packed):
+    """Config-3 shape (interleaved sessions, nonce = (s << 32) + round) through
+    the KEYED tile kernel: bit-exact vs oracle, decrypt round trip, tamper."""
+    rng = random.Random(length + packed)
+    nkeys, per = 512, 5
+    keys, s, nonces, pt, nrec = _sessions_case(rng, nkeys, per, length)
+    in_stride = length if packed else length + 32
+    out_stride = length + 16 if packed else length + 48
+    src = np.zeros(nrec * in_stride, dtype=np.uint8)
+    for r in range(nrec):
+        src[r * in_stride:r * in_stride + length] = pt[r * length:(r + 1) * length]
+    d_keys, d_idx, d_non = dev(b"".join(keys)), dev(s.view(np.uint8)), dev(nonces.view(np.uint8))
+    d_out = torch.zeros(nrec * out_stride, dtype=torch.uint8, device="cuda")
+    noise_amd.encrypt_sessions(d_keys, nkeys, d_idx, d_non, dev(src), in_stride, d_out, out_stride,
+                               length, nrec)
+    out = host(d_out)
+    for r in rng.sample(range(nrec), 200) + [0, nrec - 1]:
+        want = oracle.encrypt(keys[s[r]], int(nonces[r]), b"", pt[r * length:(r + 1) * length].tobytes())
+        assert out[r * out_stride:r * out_stride + length + 16] == want, r
+    # tamper two records, decrypt all
+    ct = bytearray(out)
+    ct[7 * out_stride + 3] ^= 1
+    ct[100 * out_stride + length] ^= 0x40  # tag byte
+    d_back = torch.full((nrec * in_stride,), 0xCD, dtype=torch.uint8, device="cuda")
+    d_st = torch.full((nrec,), 9, dtype=torch.uint8, device="cuda")
+    noise_amd.decrypt_sessions(d_keys, nkeys, d_idx, d_non, dev(bytes(ct)), out_stride, d_back, in_stride,
+                               length, d_st, nrec)
+    st = host(d_st)
+    back = host(d_back)
+    assert st[7] == noise_amd.REC_BAD_MAC and st[100] == noise_amd.REC_BAD_MAC
+    assert sum(st) == 2
+    assert back[7 * in_stride:7 * in_stride + length] == bytes(length)  # zeroed copy
+    for r in range(0, nrec, 37):
+        if r in (7, 100):
+            continue
+        assert back[r * in_stride:r * in_stride + length] == pt[r * length:(r + 1) * length].tobytes()
+
+
+def test_sessions_bad_key_index(oracle):
+    rng = random.Random(77)
+    nkeys, per, length = 64, 2, 1024
+    keys, s, nonces, pt, nrec = _sessions_case(rng, nkeys, per, length)
+    s = s.copy()
+    s[5] = nkeys + 3  # out of the table
+    d_out = torch.full((nrec * (length + 16),), 0xEE, dtype=torch.uint8, device="cuda")
+    noise_amd.encrypt_sessions(dev(b"".join(keys)), nkeys, dev(s.view(np.uint8)),
+                               dev(nonces.view(np.uint8)), dev(pt), length, d_out, length + 16,
+                               length, nrec)
+    out = host(d_out)
+    assert out[5 * 1040:6 * 1040] == b"\xee" * 1040  # not written
+    assert out[6 * 1040:7 * 1040] == oracle.encrypt(keys[s[6]], int(nonces[6]), b"",
+                                                     pt[6 * 1024:7 * 1024].tobytes())
+    d_st = torch.full((nrec,), 9, dtype=torch.uint8, device="cuda")
+    d_back = torch.zeros(nrec * length, dtype=torch.uint8, device="cuda")
+    noise_amd.decrypt_sessions(dev(b"".join(keys)), nkeys, dev(s.view(np.uint8)),
+                               dev(nonces.view(np.uint8)), d_out, length + 16, d_back, length,
+                               length, d_st, nrec)
+    st = host(d_st)
+    assert st[5] == noise_amd.REC_BAD_KEY and sum(st) == noise_amd.REC_BAD_KEY

@@ -30,10 +30,10 @@ int main() {
   };
   const dim3 g(R / 64), b(64);
   for (int rep = 0; rep < 2; ++rep) {
-    timeit("full", [&] { hipLaunchKernelGGL((k_aead_tile<false, 1024, true, 0>), g, b, 0, 0, key, 0, in, L, out, L + 16, nullptr, R, 0); });
-    timeit("no_hbm", [&] { hipLaunchKernelGGL((k_aead_tile<false, 1024, true, 1>), g, b, 0, 0, key, 0, in, L, out, L + 16, nullptr, R, 0); });
-    timeit("no_poly", [&] { hipLaunchKernelGGL((k_aead_tile<false, 1024, true, 2>), g, b, 0, 0, key, 0, in, L, out, L + 16, nullptr, R, 0); });
-    timeit("dec_full", [&] { hipLaunchKernelGGL((k_aead_tile<true, 1024, true, 0>), g, b, 0, 0, key, 0, out, L + 16, in, L, out, R, 0); });
+    timeit("full", [&] { hipLaunchKernelGGL((k_aead_tile<false, 1024, true, false, 0>), g, b, 0, 0, key, 0, in, L, out, L + 16, nullptr, R, 0, nullptr, nullptr, nullptr, 0u); });
+    timeit("no_hbm", [&] { hipLaunchKernelGGL((k_aead_tile<false, 1024, true, false, 1>), g, b, 0, 0, key, 0, in, L, out, L + 16, nullptr, R, 0, nullptr, nullptr, nullptr, 0u); });
+    timeit("no_poly", [&] { hipLaunchKernelGGL((k_aead_tile<false, 1024, true, false, 2>), g, b, 0, 0, key, 0, in, L, out, L + 16, nullptr, R, 0, nullptr, nullptr, nullptr, 0u); });
+    timeit("dec_full", [&] { hipLaunchKernelGGL((k_aead_tile<true, 1024, true, false, 0>), g, b, 0, 0, key, 0, out, L + 16, in, L, out, R, 0, nullptr, nullptr, nullptr, 0u); });
   }
   return 0;
 }

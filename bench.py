@@ -161,38 +161,8 @@ def main():
     stream = torch.cuda.current_stream()
 
     cfg = args.config
-    if cfg == 2:
-        R, L = args.records or (1 << 20), 1024
-        workload = "cfg2: 2^20 x 1 KiB records per GPU, one key, encrypt+decrypt round trip"
-        if args.records:
-            workload = "cfg2-shape: %d x 1 KiB records per GPU" % R
-        n_base = rank_nonce_base(cfg, rank, world, R, R * world)
-    elif cfg == 5:  # strong scaling: 8 Mi x 4 KiB split over the GPUs
-        total = args.records or (8 << 20)
-        lo, hi = shard(total, rank, world)
-        R, L = hi - lo, 4096
-        n_base = rank_nonce_base(cfg, rank, world, R, total)
-        workload = "cfg5: %d x 4 KiB records total, sharded over %d GPU(s)" % (total, world)
-    else:
-        raise SystemExit("configs 3/4 are parity-test shapes; bench line uses 2 (or 5)")
-    in_stride, ct_stride = L, L + 16
-
-    d_pt = torch.empty(R * L, dtype=torch.uint8, device="cuda")
-    noise_amd.fill_synthetic(d_pt, R * L, SEED, offset=n_base * L)
-    d_ct = torch.empty(R * ct_stride, dtype=torch.uint8, device="cuda")
-    d_back = torch.empty(R * L, dtype=torch.uint8, device="cuda")
-    d_st = torch.empty(R, dtype=torch.uint8, device="cuda")
-
-    def step(evs=None):
-        if evs:
-            evs[0].record(stream)
-        noise_amd.encrypt_uniform(KEY, n_base, d_pt, in_stride, d_ct, ct_stride, L, R, stream=stream)
-        if evs:
-            evs[1].record(stream)
-        noise_amd.decrypt_uniform(KEY, n_base, d_ct, ct_stride, d_back, in_stride, L, d_st, R,
-                                  stream=stream)
-        if evs:
-            evs[2].record(stream)
+    wl = make_workload(cfg, args, rank, world, stream)
+    R, L, workload, step = wl["R"], wl["L"], wl["workload"], wl["step"]
 
     log("rank %d/%d: %d records x %d B, warmup %d" % (rank, world, R, L, args.warmup))
     # correctness of the step about to be timed: all tags verify, round trip
@@ -200,8 +170,7 @@ def main():
     # the GPU clock drops -- separates the warmup from the timed steps)
     step()
     torch.cuda.synchronize()
-    ok = int(d_st.sum().item()) == 0 and torch.equal(d_pt, d_back)
-    if not ok:
+    if not wl["check"]():
         raise SystemExit("round trip failed on rank %d" % rank)
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     tw = time.perf_counter()
@@ -228,24 +197,24 @@ def main():
     else:
         total_rec = R
     # the timed work was correct too
-    if int(d_st.sum().item()) != 0 or not torch.equal(d_pt, d_back):
+    if not wl["check"]():
         raise SystemExit("timed round trip failed on rank %d" % rank)
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
     log("enc %.3f ms, dec %.3f ms per launch; step %.3f ms" %
         (enc_ms, dec_ms, elapsed * 1e3 / args.steps))
 
-    total_bytes = 2.0 * total_rec * L * args.steps  # plaintext through AEAD (enc + dec)
+    # plaintext through the AEAD (enc + dec), scaled from this rank's records
+    total_bytes = 2.0 * wl["pt_bytes"] * (total_rec / R) * args.steps
     value = total_bytes / elapsed / GIB
 
     # roofline of the dominant kernel (algorithmic bytes per launch / its
     # average duration from the HIP events on its own stream)
-    enc_bytes = R * (L + L + 16)        # read pt, write ct||tag
-    dec_bytes = R * (L + 16 + L + 1)    # read ct||tag, write pt + status byte
+    enc_bytes, dec_bytes = wl["enc_bytes"], wl["dec_bytes"]
     if enc_ms >= dec_ms:
-        kname, kbytes, kms = "k_aead_uniform<encrypt>", enc_bytes, enc_ms
+        kname, kbytes, kms = wl["knames"][0], enc_bytes, enc_ms
     else:
-        kname, kbytes, kms = "k_aead_uniform<decrypt>", dec_bytes, dec_ms
+        kname, kbytes, kms = wl["knames"][1], dec_bytes, dec_ms
     achieved = kbytes / (kms * 1e-3)
     pmc = pmc_traffic(workload)
     traffic = None
@@ -257,26 +226,180 @@ def main():
             "avg_launch_ms": round(kms, 4),
             "enc_ms": round(enc_ms, 4), "dec_ms": round(dec_ms, 4)}
 
-    line = {"metric": "GiB/s ChaChaPoly AEAD over device-resident 1 KiB Noise records, 1 & 8 GPU"
-                      if L == 1024 else "GiB/s ChaChaPoly AEAD over device-resident 4 KiB records",
+    line = {"metric": wl["metric"],
             "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
-            "higher_is_better": True, "scaling": "weak" if cfg == 2 else "strong",
+            "higher_is_better": True, "scaling": "strong" if cfg == 5 else "weak",
             "vs_baseline": None, "dtype": "u32", "data": "synthetic (splitmix64)",
-            "config": {"workload": workload, "records_per_gpu": R, "record_bytes": L,
-                       "ct_stride": ct_stride, "keys": 1, "bytes_counted":
-                       "plaintext bytes through the AEAD, encrypt + decrypt",
-                       "parallelism": "records sharded per GPU, no collective"},
+            "config": dict({"workload": workload, "records_per_gpu": R,
+                            "bytes_counted": "plaintext bytes through the AEAD, encrypt + decrypt",
+                            "parallelism": "records sharded per GPU, no collective"},
+                           **wl["config"]),
             "roofline": roof}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
         line["cpu_baseline"] = cpu_baseline()
-    if rank == 0 and args.host_inclusive:
+    if rank == 0 and args.host_inclusive and cfg == 2:
         line["host_inclusive"] = host_inclusive(R, L)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+METRIC = "GiB/s ChaChaPoly AEAD over device-resident 1 KiB Noise records, 1 & 8 GPU"
+
+
+def mix64_np(z):
+    import numpy as np
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xbf58476d1ce4e5b9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94d049bb133111eb)
+    return z ^ (z >> np.uint64(31))
+
+
+def make_workload(cfg, args, rank, world, stream):
+    """Synthetic inputs of BASELINE config `cfg`, resident in
+    HBM, and the step that runs the hot path over them once."""
+    import numpy as np
+    import torch
+    if cfg in (2, 5):
+        if cfg == 2:
+            R, L = args.records or (1 << 20), 1024
+            workload = "cfg2: 2^20 x 1 KiB records per GPU, one key, encrypt+decrypt round trip"
+            if args.records:
+                workload = "cfg2-shape: %d x 1 KiB records per GPU" % R
+            n_base = rank_nonce_base(cfg, rank, world, R, R * world)
+            metric = METRIC
+        else:  # strong scaling: 8 Mi x 4 KiB split over the GPUs
+            total = args.records or (8 << 20)
+            lo, hi = shard(total, rank, world)
+            R, L = hi - lo, 4096
+            n_base = rank_nonce_base(cfg, rank, world, R, total)
+            workload = "cfg5: %d x 4 KiB records total, sharded over %d GPU(s)" % (total, world)
+            metric = "GiB/s ChaChaPoly AEAD over device-resident 4 KiB Noise records"
+        d_pt = torch.empty(R * L, dtype=torch.uint8, device="cuda")
+        noise_amd.fill_synthetic(d_pt, R * L, SEED, offset=n_base * L)
+        d_ct = torch.empty(R * (L + 16), dtype=torch.uint8, device="cuda")
+        d_back = torch.empty(R * L, dtype=torch.uint8, device="cuda")
+        d_st = torch.empty(R, dtype=torch.uint8, device="cuda")
+
+        def step(evs=None):
+            if evs:
+                evs[0].record(stream)
+            noise_amd.encrypt_uniform(KEY, n_base, d_pt, L, d_ct, L + 16, L, R, stream=stream)
+            if evs:
+                evs[1].record(stream)
+            noise_amd.decrypt_uniform(KEY, n_base, d_ct, L + 16, d_back, L, L, d_st, R, stream=stream)
+            if evs:
+                evs[2].record(stream)
+        cfgd = {"record_bytes": L, "ct_stride": L + 16, "keys": 1}
+    elif cfg == 3:
+        # 65536 sessions x 16 records x 1 KiB, interleaved: record i belongs to
+        # session s = i mod S with nonce (s << 32) + i // S; key of session s =
+        # bytes [32s, 32s+32) of the splitmix64 stream with seed 0x4B4559.
+        S, per, L = 65536, 16, 1024
+        R = S * per
+        d_pt = torch.empty(R * L, dtype=torch.uint8, device="cuda")
+        noise_amd.fill_synthetic(d_pt, R * L, SEED, offset=rank * R * L)
+        d_keys = torch.empty(S * 32, dtype=torch.uint8, device="cuda")
+        noise_amd.fill_synthetic(d_keys, S * 32, 0x4B4559, offset=rank * S * 32)
+        i = torch.arange(R, dtype=torch.int64, device="cuda")
+        d_idx = (i % S).to(torch.int32)
+        d_non = ((i % S) << 32) + i // S
+        d_ct = torch.empty(R * (L + 16), dtype=torch.uint8, device="cuda")
+        d_back = torch.empty(R * L, dtype=torch.uint8, device="cuda")
+        d_st = torch.empty(R, dtype=torch.uint8, device="cuda")
+
+        def step(evs=None):
+            if evs:
+                evs[0].record(stream)
+            noise_amd.encrypt_sessions(d_keys, S, d_idx, d_non, d_pt, L, d_ct, L + 16, L, R,
+                                       stream=stream)
+            if evs:
+                evs[1].record(stream)
+            noise_amd.decrypt_sessions(d_keys, S, d_idx, d_non, d_ct, L + 16, d_back, L, L, d_st, R,
+                                       stream=stream)
+            if evs:
+                evs[2].record(stream)
+        workload = "cfg3: 65536 sessions x 16 records x 1 KiB per GPU, interleaved, per-record key+nonce"
+        metric = "GiB/s ChaChaPoly AEAD over device-resident 1 KiB Noise records, 64K sessions"
+        cfgd = {"record_bytes": L, "ct_stride": L + 16, "keys": S}
+    elif cfg == 4:
+        # 2^20 records of 64 * 2^k bytes, P(k) ~ 1/(k+1), k = 0..10 drawn by
+        # inverse CDF from splitmix64(seed 4); the top bucket clamped to 65519
+        # (largest Noise plaintext).  Records packed at 16-byte aligned offsets.
+        R = args.records or (1 << 20)
+        w = np.array([1.0 / (k + 1) for k in range(11)])
+        cdf = np.cumsum(w / w.sum())
+        u = mix64_np(np.uint64(4) + (np.arange(R, dtype=np.uint64) + np.uint64(1)) *
+                     np.uint64(0x9e3779b97f4a7c15)).astype(np.float64) / 2.0 ** 64
+        k = np.minimum(np.searchsorted(cdf, u, side="right"), 10)
+        lens = np.minimum(64 << k, 65519).astype(np.uint64)
+        in_sz = (lens + np.uint64(15)) // np.uint64(16) * np.uint64(16)
+        ct_sz = (lens + np.uint64(31)) // np.uint64(16) * np.uint64(16)
+        in_off = np.concatenate([[0], np.cumsum(in_sz)[:-1]]).astype(np.uint64)
+        ct_off = np.concatenate([[0], np.cumsum(ct_sz)[:-1]]).astype(np.uint64)
+        n_base = rank * R
+        enc_d = np.zeros(R, dtype=noise_amd.record_dtype())
+        enc_d["in_off"], enc_d["out_off"] = in_off, ct_off
+        enc_d["nonce"] = np.arange(R, dtype=np.uint64) + np.uint64(n_base)
+        enc_d["len"] = lens
+        dec_d = enc_d.copy()
+        dec_d["in_off"], dec_d["out_off"] = ct_off, in_off
+        tot_in, tot_ct = int(in_sz.sum()), int(ct_sz.sum())
+        d_pt = torch.empty(tot_in, dtype=torch.uint8, device="cuda")
+        noise_amd.fill_synthetic(d_pt, tot_in, SEED)
+        d_ct = torch.empty(tot_ct, dtype=torch.uint8, device="cuda")
+        d_back = torch.empty(tot_in, dtype=torch.uint8, device="cuda")
+        d_st = torch.empty(R, dtype=torch.uint8, device="cuda")
+        d_key = torch.frombuffer(bytearray(KEY), dtype=torch.uint8).cuda()
+        d_enc = torch.from_numpy(enc_d.view(np.uint8).copy()).cuda()
+        d_dec = torch.from_numpy(dec_d.view(np.uint8).copy()).cuda()
+        L = int(lens.sum() // R)
+
+        def step(evs=None):
+            if evs:
+                evs[0].record(stream)
+            noise_amd.encrypt_records(d_key, 1, d_enc, R, d_pt, d_ct, stream=stream)
+            if evs:
+                evs[1].record(stream)
+            noise_amd.decrypt_records(d_key, 1, d_dec, R, d_ct, d_back, d_st, stream=stream)
+            if evs:
+                evs[2].record(stream)
+        workload = "cfg4: 2^20 records per GPU, 64 B .. 65519 B (P(k) ~ 1/(k+1)), one key"
+        metric = "GiB/s ChaChaPoly AEAD over device-resident mixed-size Noise records"
+        cfgd = {"mean_record_bytes": L, "total_plaintext_bytes": int(lens.sum()), "keys": 1}
+        pt_bytes = int(lens.sum())
+        lens_t = torch.from_numpy(lens.astype(np.int64)).cuda()
+        off_t = torch.from_numpy(in_off.astype(np.int64)).cuda()
+
+        def check():
+            if int(d_st.sum().item()) != 0:
+                return False
+            # sampled exact comparison of whole records (the padding is not a record byte)
+            idx = torch.randint(0, R, (4096,), device="cuda")
+            for r in idx.tolist()[:256]:
+                o, n = int(off_t[r]), int(lens_t[r])
+                if not torch.equal(d_pt[o:o + n], d_back[o:o + n]):
+                    return False
+            return True
+        return {"R": R, "L": L, "workload": workload, "step": step, "check": check,
+                "metric": metric, "config": cfgd, "pt_bytes": pt_bytes,
+                "enc_bytes": pt_bytes + int((lens + 16).sum()) + 48 * R,
+                "dec_bytes": pt_bytes + int((lens + 16).sum()) + 49 * R,
+                "knames": ("k_aead_records<encrypt>", "k_aead_records<decrypt>")}
+    else:
+        raise SystemExit("unknown config %d" % cfg)
+
+    def check():
+        return int(d_st.sum().item()) == 0 and torch.equal(d_pt, d_back)
+    return {"R": R, "L": L, "workload": workload, "step": step, "check": check,
+            "metric": metric, "config": cfgd, "pt_bytes": R * L,
+            # cfg 3 also reads a 4-B key index + 8-B nonce per record and the key table
+            "enc_bytes": R * (2 * L + 16) + ((12 * R + 32 * 65536) if cfg == 3 else 0),
+            "dec_bytes": R * (2 * L + 17) + ((12 * R + 32 * 65536) if cfg == 3 else 0),
+            "knames": ("k_aead_sessions<encrypt>", "k_aead_sessions<decrypt>") if cfg == 3 else
+                      ("k_aead_uniform<encrypt>", "k_aead_uniform<decrypt>")}
 
 
 def host_inclusive(R, L):

@@ -85,8 +85,10 @@ int noise_gpu_device_count(int *count);
  * record whose tag fails is left as it was when in-place (the reference
  * leaves the buffer untouched, monocypher.c:2919-2926) and is zeroed in an
  * out-of-place output (no unauthenticated plaintext is left behind).
- * Records are processed one per lane; 16-byte aligned pointers/strides and
- * len % 16 == 0 take the vector path, anything else a byte-granular path. */
+ * 16-byte aligned pointers/strides, ad_len == 0 and len in {64, 128, 192,
+ * 256, 512, 1024, 2048, 4096, 8192, 16384} run on the LDS-staged tile kernel
+ * (the hot path); other shapes one record per lane (vector path when 16-byte
+ * aligned with len % 16 == 0, byte-granular otherwise). */
 int noise_gpu_encrypt_uniform(const uint8_t h_key[32], uint64_t nonce0,
                               const uint8_t *d_in, uint64_t in_stride,
                               uint8_t *d_out, uint64_t out_stride,
@@ -102,8 +104,17 @@ int noise_gpu_decrypt_uniform(const uint8_t h_key[32], uint64_t nonce0,
                               uint8_t *d_status, uint64_t nrec, void *stream);
 
 /* ---- device-resident descriptor batches (many sessions, mixed sizes) ---
- * d_keys: [nkeys][32] key table in HBM; d_recs: nrec descriptors in HBM.
- * Same in-place / failure rules as the uniform functions. */
+ * d_keys: [nkeys][32] key table in HBM (16-byte aligned); d_recs: nrec
+ * descriptors in HBM.  Same in-place / failure rules as the uniform
+ * functions; a record is in place when d_in + in_off == d_out + out_off.
+ * A descriptor whose key_idx >= nkeys is not processed (nothing written;
+ * decrypt status NOISE_GPU_REC_BAD_KEY).
+ * Batches of >= 2048 records are load-balanced on the device, stream-ordered
+ * (no host synchronisation): records are sorted by class and each class
+ * runs its own kernel -- 16-byte aligned AD-free records of 64..16384 bytes
+ * (powers of two and 192) on the LDS-staged tile kernel, aligned AD-free
+ * records longer than 16 KiB one wavefront per record, everything else one
+ * lane per record.  Scratch comes from a per-device stream-ordered pool. */
 int noise_gpu_encrypt_records(const uint8_t *d_keys, uint32_t nkeys,
                               const noise_gpu_record *d_recs, uint64_t nrec,
                               const uint8_t *d_in, uint8_t *d_out,
@@ -121,7 +132,7 @@ int noise_gpu_decrypt_records(const uint8_t *d_keys, uint32_t nkeys,
  * nonce d_nonces[i]; records laid out like the uniform batches (d_in + i *
  * in_stride, d_out + i * out_stride).  No associated data (transport).
  * Served by the LDS-staged tile kernel: len in {64, 128, 192, 256, 512,
- * 1024, 2048, 4096} with 16-byte aligned buffers/strides; other shapes
+ * 1024, 2048, 4096, 8192, 16384} with 16-byte aligned buffers/strides; other shapes
  * return NOISE_GPU_E_ARG (use the descriptor functions below).  A record
  * whose key index is >= nkeys is not written; decrypt marks it
  * NOISE_GPU_REC_BAD_KEY. */

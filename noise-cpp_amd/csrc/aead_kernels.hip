@@ -4,8 +4,7 @@
 //   k_encrypt_uniform / k_decrypt_uniform   one key, fixed length, implicit
 //                                            nonce0 + i, fixed strides (the
 //                                            BASELINE config-2 hot path)
-//   k_encrypt_records / k_decrypt_records   descriptor batches: per-record
-//                                            key row, nonce, length, offsets
+//   (descriptor batches: records_kernels.hip)
 //   k_rekey                                  CipherState::rekey on a table
 //   k_fill_synthetic                         splitmix64 test/bench data
 //
@@ -33,33 +32,6 @@ __global__ __launch_bounds__(kBlock) void k_aead_uniform(
   const bool ok = aead_record<DECRYPT, VEC>(
       k, nonce0 + i, in + i * in_stride, out + i * out_stride, len,
       ad + i * ad_stride, ad_len);
-  if (DECRYPT) status[i] = ok ? 0u : 1u;
-}
-
-template <bool DECRYPT>
-__global__ __launch_bounds__(kBlock) void k_aead_records(
-    const uint8_t *__restrict__ keys, uint32_t nkeys,
-    const noise_gpu_record *__restrict__ recs, uint64_t nrec,
-    const uint8_t *in, uint8_t *out, const uint8_t *ad, uint8_t *status) {
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= nrec) return;
-  const noise_gpu_record r = recs[i];
-  if (r.key_idx >= nkeys) {  // host validated; never index out of the table
-    if (DECRYPT) status[i] = 1u;
-    return;
-  }
-  const uint4 *kp = reinterpret_cast<const uint4 *>(keys + 32u * r.key_idx);
-  const uint4 ka = kp[0], kb = kp[1];
-  const uint32_t k[8] = {ka.x, ka.y, ka.z, ka.w, kb.x, kb.y, kb.z, kb.w};
-  const uint8_t *src = in + r.in_off;
-  uint8_t *dst = out + r.out_off;
-  const bool vec = ((reinterpret_cast<uintptr_t>(src) |
-                     reinterpret_cast<uintptr_t>(dst) | r.len) & 15u) == 0;
-  bool ok;
-  if (vec)
-    ok = aead_record<DECRYPT, true>(k, r.nonce, src, dst, r.len, ad + r.ad_off, r.ad_len);
-  else
-    ok = aead_record<DECRYPT, false>(k, r.nonce, src, dst, r.len, ad + r.ad_off, r.ad_len);
   if (DECRYPT) status[i] = ok ? 0u : 1u;
 }
 
@@ -124,13 +96,22 @@ hipError_t launch_aead_uniform(bool decrypt, const uint32_t key[8],
                      out_stride | len) & 15u) == 0;
   // LDS-staged tile kernel: aligned, AD-free, supported lengths
   if (vec && ad_len == 0) {
-    const int in_place = in == out;
+    TileArgs ta{};
+    ta.key = k;
+    ta.nonce0 = nonce0;
+    ta.in = in;
+    ta.in_stride = in_stride;
+    ta.out = out;
+    ta.out_stride = out_stride;
+    ta.status = status;
+    ta.nrec = nrec;
+    ta.in_place = in == out;
     const dim3 gt((unsigned)((nrec + 63) / 64)), bt(64);
     // packed records (stride == record size on both sides): cheap addressing
     const bool contig = decrypt ? (in_stride == (uint64_t)len + 16 && out_stride == len)
                                 : (in_stride == len && out_stride == (uint64_t)len + 16);
 #define NOISE_TILE_LAUNCH(DEC, LEN, CONTIG)                                    \
-    hipLaunchKernelGGL((k_aead_tile<DEC, LEN, CONTIG>), gt, bt, 0, stream, k, nonce0, in, in_stride, out, out_stride, status, nrec, in_place, nullptr, nullptr, nullptr, 0u)
+    hipLaunchKernelGGL((k_aead_tile<DEC, LEN, CONTIG>), gt, bt, 0, stream, ta)
 #define NOISE_TILE_CASE(LEN)                                                   \
     case LEN:                                                                  \
       if (decrypt) {                                                           \
@@ -150,6 +131,8 @@ hipError_t launch_aead_uniform(bool decrypt, const uint32_t key[8],
       NOISE_TILE_CASE(1024)
       NOISE_TILE_CASE(2048)
       NOISE_TILE_CASE(4096)
+      NOISE_TILE_CASE(8192)
+      NOISE_TILE_CASE(16384)
       default: break;
     }
 #undef NOISE_TILE_CASE
@@ -167,20 +150,6 @@ hipError_t launch_aead_uniform(bool decrypt, const uint32_t key[8],
     else
       hipLaunchKernelGGL((k_aead_uniform<false, false>), g, b, 0, stream, k, nonce0, in, in_stride, out, out_stride, len, ad, ad_stride, ad_len, status, nrec);
   }
-  return hipGetLastError();
-}
-
-hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
-                               uint32_t nkeys, const noise_gpu_record *recs,
-                               uint64_t nrec, const uint8_t *in, uint8_t *out,
-                               const uint8_t *ad, uint8_t *status,
-                               hipStream_t stream) {
-  if (nrec == 0) return hipSuccess;
-  const dim3 g = grid_for(nrec), b(kBlock);
-  if (decrypt)
-    hipLaunchKernelGGL((k_aead_records<true>), g, b, 0, stream, keys, nkeys, recs, nrec, in, out, ad, status);
-  else
-    hipLaunchKernelGGL((k_aead_records<false>), g, b, 0, stream, keys, nkeys, recs, nrec, in, out, ad, status);
   return hipGetLastError();
 }
 

@@ -284,7 +284,29 @@ __device__ __forceinline__ F26 mul26(const F26 &x, const F26 &y) {
 }
 
 // ---------------------------------------------------------------- memory
+// Wave-uniform 32-bit value into an SGPR.  The builtin returns a signed
+// int: widening it directly sign-extends (an offset >= 2^31 would turn
+// into a wild address), so it is always taken as uint32_t here.
+__device__ __forceinline__ uint32_t uniform32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ uint64_t join64(uint32_t hi, uint32_t lo) {
+  return ((uint64_t)hi << 32) | (uint64_t)lo;
+}
+
+// Explicit memory waits (s_waitcnt simm16, gfx9 layout: vmcnt in [3:0] and
+// [15:14], expcnt [6:4], lgkmcnt [11:8]; a field at its maximum = no wait).
+// Callers follow each with wave_lds_fence() to pin LDS accesses around it.
+__device__ __forceinline__ void wait_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
+__device__ __forceinline__ void wait_lds() { __builtin_amdgcn_s_waitcnt(0xC07F); }   // lgkmcnt(0)
+__device__ __forceinline__ void wait_all() { __builtin_amdgcn_s_waitcnt(0x0070); }   // both
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// Record buffers are device (global) memory.  Naming the address space keeps
+// the compiler from falling back to FLAT instructions when it cannot trace a
+// pointer to a kernel argument (e.g. base + an offset read from a
+// descriptor); FLAT stores also count against lgkmcnt.
+typedef __attribute__((address_space(1))) u32x4 g_u32x4;
 
 // Byte-granular little-endian word load/store for unaligned records.
 __device__ __forceinline__ uint32_t ld_bytes(const uint8_t *p, int n) {
@@ -302,7 +324,7 @@ template <bool VEC>
 __device__ __forceinline__ uint4 load16(const uint8_t *p, int n) {
   if (VEC) {
     // one global_load_dwordx4; records are streamed once (nontemporal)
-    const u32x4 w = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+    const u32x4 w = __builtin_nontemporal_load((const g_u32x4 *)p);
     return make_uint4(w.x, w.y, w.z, w.w);
   }
   uint4 v;
@@ -318,7 +340,7 @@ __device__ __forceinline__ void store16(uint8_t *p, uint4 v, int n) {
     // one aligned global_store_dwordx4 (a plain uint4 store may be
     // re-split by the store merger into misaligned dwordx3/x4 pieces)
     const u32x4 w = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(w, reinterpret_cast<u32x4 *>(p));
+    __builtin_nontemporal_store(w, (g_u32x4 *)p);
     return;
   }
   st_bytes(p, v.x, n >= 4 ? 4 : n);

@@ -232,7 +232,7 @@ static int sessions(bool decrypt, const uint8_t *d_keys, uint32_t nkeys,
                          nullptr, 0, d_status, nrec);
   if (rc) return rc;
   if (!noise_amd::sessions_supported(len, d_in, in_stride, d_out, out_stride))
-    return arg_fail("sessions batches need len in {64,128,192,256,512,1024,2048,4096} "
+    return arg_fail("sessions batches need len in {64,128,192,256,512,1024,2048,4096,8192,16384} "
                     "and 16-byte aligned buffers/strides");
   if ((rc = check_device())) return rc;
   HIP_TRY(noise_amd::launch_aead_sessions(decrypt, d_keys, nkeys, d_key_idx,

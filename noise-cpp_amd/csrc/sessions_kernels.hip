@@ -16,7 +16,8 @@ bool sessions_supported(uint32_t len, const void *in, uint64_t in_stride,
                      reinterpret_cast<uintptr_t>(out) | in_stride |
                      out_stride | len) & 15u) == 0;
   switch (len) {
-    case 64: case 128: case 192: case 256: case 512: case 1024: case 2048: case 4096:
+    case 64: case 128: case 192: case 256: case 512: case 1024: case 2048:
+    case 4096: case 8192: case 16384:
       return vec;
     default:
       return false;
@@ -31,13 +32,23 @@ hipError_t launch_aead_sessions(bool decrypt, const uint8_t *keys,
                                 uint8_t *status, uint64_t nrec,
                                 hipStream_t stream) {
   if (nrec == 0) return hipSuccess;
-  const KeyArg k{};
-  const int in_place = in == out;
+  TileArgs ta{};
+  ta.in = in;
+  ta.in_stride = in_stride;
+  ta.out = out;
+  ta.out_stride = out_stride;
+  ta.status = status;
+  ta.nrec = nrec;
+  ta.in_place = in == out;
+  ta.keys = keys;
+  ta.nkeys = nkeys;
+  ta.key_idx = key_idx;
+  ta.nonces = nonces;
   const dim3 gt((unsigned)((nrec + 63) / 64)), bt(64);
   const bool contig = decrypt ? (in_stride == (uint64_t)len + 16 && out_stride == len)
                               : (in_stride == len && out_stride == (uint64_t)len + 16);
 #define NOISE_SESS_LAUNCH(DEC, LEN, CONTIG)                                    \
-    hipLaunchKernelGGL((k_aead_tile<DEC, LEN, CONTIG, true>), gt, bt, 0, stream, k, 0, in, in_stride, out, out_stride, status, nrec, in_place, keys, key_idx, nonces, nkeys)
+    hipLaunchKernelGGL((k_aead_tile<DEC, LEN, CONTIG, kTileSessions>), gt, bt, 0, stream, ta)
 #define NOISE_SESS_CASE(LEN)                                                   \
     case LEN:                                                                  \
       if (decrypt) {                                                           \
@@ -57,6 +68,8 @@ hipError_t launch_aead_sessions(bool decrypt, const uint8_t *keys,
     NOISE_SESS_CASE(1024)
     NOISE_SESS_CASE(2048)
     NOISE_SESS_CASE(4096)
+    NOISE_SESS_CASE(8192)
+    NOISE_SESS_CASE(16384)
     default:
       return hipErrorInvalidValue;
   }

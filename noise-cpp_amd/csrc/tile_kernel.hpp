@@ -42,12 +42,21 @@ struct TileCfg {
   static constexpr int SPR = L / 16;                // 16-B slots per record
   static constexpr int REC_SLOTS = RPT * SPR;
   static constexpr int NSLOT = REC_SLOTS + RPT;     // + one tag slot per record
-  static constexpr int LOG2G = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : 4;
+  static constexpr int LOG2G = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3
+                              : G == 16 ? 4 : G == 32 ? 5 : 6;
   static_assert(L % 64 == 0 && 64 % G == 0 && (L < 256 || L % 256 == 0), "tile shape");
 };
 
 // slot <-> piece involution inside each aligned 16-slot group
 __device__ __forceinline__ uint32_t swz(uint32_t s) { return s ^ ((s >> 4) & 15u); }
+
+// LDS-typed pointer for the LDS-DMA destinations.  Taking it straight from
+// the __shared__ array (instead of casting a generic pointer inside a
+// helper) keeps the address space static: a generic->LDS cast that the
+// compiler cannot fold makes ROCm 7.2's gfx950 backend emit an illegal
+// V_CMP on src_shared_base when many kernels share one module.
+typedef __attribute__((address_space(3))) uint4 lds_u4;
+#define NOISE_LDS3(arr) ((lds_u4 *)(arr))
 
 // compiler-level LDS ordering point for a single-wave workgroup
 __device__ __forceinline__ void wave_lds_fence() {
@@ -55,11 +64,48 @@ __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_wave_barrier();
 }
 
-template <int L, bool DECRYPT, bool CONTIG, int ABL>
-__device__ __forceinline__ void tile_load(uint4 *lds, const uint8_t *in,
+// Record addressing / keying of a tile launch.
+enum TileMode : int {
+  kTileUniform = 0,   // one key, nonce0 + i, record i at in + i*in_stride
+  kTileSessions = 1,  // key row keys[key_idx[i]], nonce nonces[i], strided
+  kTileDesc = 2,      // descriptor recs[idx[base + i]] (records API class)
+};
+
+struct TileArgs {
+  KeyArg key;         // kTileUniform
+  uint64_t nonce0;    // kTileUniform
+  const uint8_t *in;
+  uint64_t in_stride;  // kTileUniform / kTileSessions
+  uint8_t *out;
+  uint64_t out_stride;
+  uint8_t *status;    // decrypt: per record (kTileDesc: per descriptor)
+  uint64_t nrec;      // kTileUniform / kTileSessions
+  int in_place;       // kTileUniform / kTileSessions
+  uint32_t nkeys;     // kTileSessions / kTileDesc
+  const uint8_t *keys;
+  const uint32_t *key_idx;  // kTileSessions
+  const uint64_t *nonces;   // kTileSessions
+  const noise_gpu_record *recs;  // kTileDesc
+  const uint32_t *idx;           // kTileDesc: class-sorted descriptor indices
+  const unsigned long long *counts;  // kTileDesc: per-class counts (device)
+  int cls;                       // kTileDesc: this launch's class
+};
+
+// kTileDesc: the class's slice of the sorted index array
+__device__ __forceinline__ void desc_class_range(const TileArgs &a,
+                                                 uint64_t &base, uint64_t &n) {
+  base = 0;
+  for (int c = 0; c < a.cls; ++c) base += a.counts[c];
+  n = a.counts[a.cls];
+}
+
+template <int L, bool DECRYPT, bool CONTIG, int MODE, int ABL>
+__device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
                                           uint64_t in_stride, uint64_t rec0,
                                           uint32_t nv, uint32_t lane,
-                                          const uint32_t gl[4]) {
+                                          const uint32_t gl[4],
+                                          uint32_t t_rpt, uint32_t own_in_lo,
+                                          uint32_t own_in_hi) {
   using C = TileCfg<L>;
   if (ABL == 1) return;
   constexpr int IN_SLOTS = DECRYPT ? C::NSLOT : C::REC_SLOTS;
@@ -76,7 +122,7 @@ __device__ __forceinline__ void tile_load(uint4 *lds, const uint8_t *in,
       if (rr < nv)
         __builtin_amdgcn_global_load_lds(
             (const void *)(base + off),
-            (__attribute__((address_space(3))) void *)(lds + 64 * q), 16, 0, 0);
+            (__attribute__((address_space(3))) void *)(lds3 + 64 * q), 16, 0, 0);
     }
     if (DECRYPT) {  // tag pieces: slot REC_SLOTS + r <- piece (r, SPR)
 #pragma unroll
@@ -85,7 +131,7 @@ __device__ __forceinline__ void tile_load(uint4 *lds, const uint8_t *in,
         if (r < nv)
           __builtin_amdgcn_global_load_lds(
               (const void *)(base + 16u * (r * (C::SPR + 1) + C::SPR)),
-              (__attribute__((address_space(3))) void *)(lds + 64 * q), 16, 0, 0);
+              (__attribute__((address_space(3))) void *)(lds3 + 64 * q), 16, 0, 0);
       }
     }
   } else {
@@ -101,36 +147,48 @@ __device__ __forceinline__ void tile_load(uint4 *lds, const uint8_t *in,
         r = s - C::REC_SLOTS;
         p = C::SPR;
       }
+      const uint8_t *rec_base;
+      if (MODE == kTileDesc) {  // record r's offset lives in key lane t*RPT + r
+        const uint32_t src = t_rpt + (r < (uint32_t)C::RPT ? r : 0u);
+        const uint64_t off = ((uint64_t)(uint32_t)__shfl((int)own_in_hi, src) << 32) |
+                             (uint32_t)__shfl((int)own_in_lo, src);
+        rec_base = in + off;
+      } else {
+        rec_base = in + (rec0 + r) * in_stride;
+      }
       if (s < (uint32_t)IN_SLOTS && r < nv)
         __builtin_amdgcn_global_load_lds(
-            (const void *)(in + (rec0 + r) * in_stride + 16u * p),
-            (__attribute__((address_space(3))) void *)(lds + 64 * q), 16, 0, 0);
+            (const void *)(rec_base + 16u * p),
+            (__attribute__((address_space(3))) void *)(lds3 + 64 * q), 16, 0, 0);
     }
   }
 }
 
-// KEYED = true ("sessions" batch): record i uses key row
-// s_keys[s_key_idx[i]] and nonce s_nonces[i]; a key index outside the table
-// makes the record fail (nothing written; decrypt status 2).
+// MODE kTileSessions / kTileDesc: record i uses key row keys[key_idx] and
+// its own nonce; a key index outside the table makes the record fail
+// (nothing written; decrypt status NOISE_GPU_REC_BAD_KEY).  kTileDesc also
+// takes per-record offsets from the descriptor (16-byte aligned; the
+// classifier guarantees it) and is launched with a capped grid that strides
+// over the class's super-tiles.
 // ABL (ablation, tools/ubench only; the product uses 0): 1 = no HBM traffic
 // (compute on whatever the LDS holds), 2 = no Poly1305 work.
-template <bool DECRYPT, int L, bool CONTIG, bool KEYED = false, int ABL = 0>
-__global__ __launch_bounds__(64) void k_aead_tile(
-    KeyArg key, uint64_t nonce0, const uint8_t *in, uint64_t in_stride,
-    uint8_t *out, uint64_t out_stride, uint8_t *status, uint64_t nrec,
-    int in_place, const uint8_t *__restrict__ s_keys,
-    const uint32_t *__restrict__ s_key_idx, const uint64_t *__restrict__ s_nonces,
-    uint32_t s_nkeys) {
+template <bool DECRYPT, int L, bool CONTIG, int MODE = kTileUniform, int ABL = 0>
+__global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
   using C = TileCfg<L>;
+  constexpr bool KEYED = MODE != kTileUniform;
   constexpr int OPR = DECRYPT ? C::SPR : C::SPR + 1;  // out pieces / record
   constexpr int OUT_SLOTS = C::RPT * OPR;
   constexpr int NOUT = (OUT_SLOTS + 63) / 64;          // store instructions
+  static_assert(!(CONTIG && MODE == kTileDesc), "descriptor tiles are strided");
   __shared__ uint4 lds[C::NSLOT];
   const uint32_t lane = threadIdx.x;
-  const uint64_t super0 = (uint64_t)blockIdx.x * 64;
+  const uint8_t *in = a.in;
+  uint8_t *out = a.out;
+  uint64_t nrec = a.nrec, dbase = 0;
+  if (MODE == kTileDesc) desc_class_range(a, dbase, nrec);
   uint32_t k[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) k[i] = key.w[i];
+  for (int i = 0; i < 8; ++i) k[i] = a.key.w[i];
 
   const uint32_t rho = lane / C::G, j = lane % C::G;
   // swz(64q + lane) - 64q depends on q only through q & 3
@@ -138,32 +196,40 @@ __global__ __launch_bounds__(64) void k_aead_tile(
 #pragma unroll
   for (int i = 0; i < 4; ++i) gl[i] = swz(64u * i + lane) - 64u * i;
 
-  // the first tile's DMA goes out before the key pass and lands meanwhile
-  {
-    const uint64_t left = nrec - super0;
-    tile_load<L, DECRYPT, CONTIG, ABL>(lds, in, in_stride, super0,
-                                       left < (uint64_t)C::RPT ? (uint32_t)left : C::RPT,
-                                       lane, gl);
-  }
-
+#pragma unroll 1
+  for (uint64_t super0 = (uint64_t)blockIdx.x * 64; super0 < nrec;
+       super0 += (uint64_t)gridDim.x * 64) {
   // ---- key pass: lane l -> one-time key of record super0 + l -------------
   uint32_t kr[4], kss[4];
   F26 pw[C::LOG2G > 0 ? C::LOG2G : 1];
-  uint32_t own_k[8], own_nlo = 0, own_nhi = 0;  // KEYED: this lane's record
-  bool own_bad = false;
+  uint32_t own_k[8], own_nlo = 0, own_nhi = 0;  // keyed modes: this lane's record
+  uint32_t own_in_lo = 0, own_in_hi = 0, own_out_lo = 0, own_out_hi = 0, own_di = 0;
+  bool own_bad = false, own_inplace = false;
   {
-    uint64_t n = nonce0 + super0 + lane;
+    uint64_t n = a.nonce0 + super0 + lane;
     if (KEYED) {
       const uint64_t rec = super0 + lane;
       uint32_t ki = 0;
       n = 0;
       if (rec < nrec) {
-        ki = __builtin_nontemporal_load(s_key_idx + rec);
-        n = __builtin_nontemporal_load(s_nonces + rec);
+        if (MODE == kTileSessions) {
+          ki = __builtin_nontemporal_load(a.key_idx + rec);
+          n = __builtin_nontemporal_load(a.nonces + rec);
+        } else {
+          own_di = a.idx[dbase + rec];
+          const noise_gpu_record d = a.recs[own_di];
+          ki = d.key_idx;
+          n = d.nonce;
+          own_in_lo = (uint32_t)d.in_off;
+          own_in_hi = (uint32_t)(d.in_off >> 32);
+          own_out_lo = (uint32_t)d.out_off;
+          own_out_hi = (uint32_t)(d.out_off >> 32);
+          own_inplace = in + d.in_off == out + d.out_off;
+        }
       }
-      own_bad = ki >= s_nkeys;
+      own_bad = ki >= a.nkeys;
       if (own_bad) ki = 0;
-      const u32x4 *kp = reinterpret_cast<const u32x4 *>(s_keys + 32ull * ki);
+      const u32x4 *kp = reinterpret_cast<const u32x4 *>(a.keys + 32ull * ki);
       const u32x4 ka = __builtin_nontemporal_load(kp), kb = __builtin_nontemporal_load(kp + 1);
       own_k[0] = ka.x; own_k[1] = ka.y; own_k[2] = ka.z; own_k[3] = ka.w;
       own_k[4] = kb.x; own_k[5] = kb.y; own_k[6] = kb.z; own_k[7] = kb.w;
@@ -172,6 +238,14 @@ __global__ __launch_bounds__(64) void k_aead_tile(
     } else {
 #pragma unroll
       for (int i = 0; i < 8; ++i) own_k[i] = k[i];
+    }
+    // the first tile's DMA goes out before the key pass and lands meanwhile
+    {
+      const uint64_t left = nrec - super0;
+      tile_load<L, DECRYPT, CONTIG, MODE, ABL>(
+          NOISE_LDS3(lds), in, a.in_stride, super0,
+          left < (uint64_t)C::RPT ? (uint32_t)left : C::RPT, lane, gl, 0u,
+          own_in_lo, own_in_hi);
     }
     uint32_t otk[16];
     chacha20_block(own_k, 0u, (uint32_t)n, (uint32_t)(n >> 32), otk);
@@ -199,7 +273,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(
     const uint32_t nv = (nrec - rec0) < (uint64_t)C::RPT ? (uint32_t)(nrec - rec0) : C::RPT;
 
     // this tile's DMA (and the previous tile's stores) must have landed
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wait_vmem();
     wave_lds_fence();
 
     // ---- per-lane record work -------------------------------------------
@@ -226,7 +300,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(
       n_hi = __shfl(own_nhi, src);
       bad_key = __shfl((int)own_bad, src) != 0;
     } else {
-      const uint64_t n = nonce0 + rec0 + rho;
+      const uint64_t n = a.nonce0 + rec0 + rho;
       n_lo = (uint32_t)n;
       n_hi = (uint32_t)(n >> 32);
     }
@@ -278,6 +352,9 @@ __global__ __launch_bounds__(64) void k_aead_tile(
       }
 #pragma unroll
       for (int b = 0; b < C::LOG2G; ++b) {
+        // limbs are < 2^26 + 2^9 after mul26: 16 of them fit in 32 bits,
+        // 64 do not, so wide records re-normalise halfway
+        if (b == 4) carry26(h);
 #pragma unroll
         for (int i = 0; i < 5; ++i) h.a[i] += __shfl_xor(h.a[i], 1 << b);
       }
@@ -292,15 +369,24 @@ __global__ __launch_bounds__(64) void k_aead_tile(
     uint64_t fail_mask = 0;  // bit (r * G): record r of this tile is not output
     const uint64_t badk_mask = KEYED ? __ballot(j == 0 && bad_key) : 0ull;
     fail_mask = badk_mask;
+    // cross-lane reads stay outside divergent code: a ds_bpermute from a lane
+    // that is inactive does not return that lane's value
+    const uint32_t rec_di = MODE == kTileDesc ? (uint32_t)__shfl((int)own_di, src) : 0u;
+    const bool rec_inplace = MODE == kTileDesc ? __shfl((int)own_inplace, src) != 0 : false;
     if (DECRYPT) {
       const uint4 want = lds[C::REC_SLOTS + rho];
       const uint32_t diff = (want.x ^ tag[0]) | (want.y ^ tag[1]) |
                             (want.z ^ tag[2]) | (want.w ^ tag[3]);
       fail_mask |= __ballot(j == 0 && diff != 0u);
-      if (j == 0 && valid) status[rec0 + rho] = bad_key ? 2u : (diff ? 1u : 0u);
+      if (j == 0 && valid) {
+        const uint64_t si = MODE == kTileDesc ? (uint64_t)rec_di : rec0 + rho;
+        a.status[si] = bad_key ? 2u : (diff ? 1u : 0u);
+      }
     } else if (j == 0) {
       lds[C::REC_SLOTS + rho] = make_uint4(tag[0], tag[1], tag[2], tag[3]);
     }
+    // kTileDesc: a failed in-place record is kept, a failed copy is zeroed
+    const uint64_t inpl_mask = MODE == kTileDesc ? __ballot(j == 0 && rec_inplace) : 0ull;
     wave_lds_fence();
 
     // ---- gather this tile's output records into registers ----------------
@@ -320,11 +406,13 @@ __global__ __launch_bounds__(64) void k_aead_tile(
         // failed tag (decrypt): keep an in-place record, zero a copy;
         // invalid key index: write nothing
         const bool bad_key_rec = KEYED && ((badk_mask >> (r * C::G)) & 1u);
-        st[q] = st[q] && DECRYPT && !in_place && !bad_key_rec;
+        const bool inpl = MODE == kTileDesc ? ((inpl_mask >> (r * C::G)) & 1u) != 0
+                                            : a.in_place != 0;
+        st[q] = st[q] && DECRYPT && !inpl && !bad_key_rec;
         ov[q] = make_uint4(0u, 0u, 0u, 0u);
       }
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS reads done
+    wait_lds();  // LDS reads done
     wave_lds_fence();
 
     // ---- next tile's DMA, then this tile's stores: both in flight at once
@@ -332,9 +420,10 @@ __global__ __launch_bounds__(64) void k_aead_tile(
       const uint64_t nrec0 = rec0 + C::RPT;
       if (nrec0 < nrec) {
         const uint64_t left = nrec - nrec0;
-        tile_load<L, DECRYPT, CONTIG, ABL>(lds, in, in_stride, nrec0,
-                                           left < (uint64_t)C::RPT ? (uint32_t)left : C::RPT,
-                                           lane, gl);
+        tile_load<L, DECRYPT, CONTIG, MODE, ABL>(
+            NOISE_LDS3(lds), in, a.in_stride, nrec0,
+            left < (uint64_t)C::RPT ? (uint32_t)left : C::RPT, lane, gl,
+            (uint32_t)(t + 1) * C::RPT, own_in_lo, own_in_hi);
       }
     }
 #pragma unroll
@@ -343,12 +432,20 @@ __global__ __launch_bounds__(64) void k_aead_tile(
       const uint32_t r = g / OPR, pc = g % OPR;
       bool store = st[q];
       if (ABL == 1) store = store && (ov[q].x == 0x12345678u && ov[q].y == 0x9abcdef0u);
-      if (store) {
-        const uint64_t off = CONTIG ? 16ull * g : r * out_stride + 16u * pc;
-        store16<true>(out + rec0 * out_stride + off, ov[q], 16);
+      uint8_t *dst;
+      if (MODE == kTileDesc) {
+        const uint32_t rs = (uint32_t)t * C::RPT + (r < (uint32_t)C::RPT ? r : 0u);
+        const uint64_t off = ((uint64_t)(uint32_t)__shfl((int)own_out_hi, rs) << 32) |
+                             (uint32_t)__shfl((int)own_out_lo, rs);
+        dst = out + off + 16u * pc;
+      } else {
+        dst = out + rec0 * a.out_stride +
+              (CONTIG ? 16ull * g : r * a.out_stride + 16u * pc);
       }
+      if (store) store16<true>(dst, ov[q], 16);
     }
   }
+  }  // super-tiles (one iteration unless the grid is capped: kTileDesc)
 }
 
 }  // namespace noise_amd

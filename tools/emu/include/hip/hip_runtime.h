@@ -1,0 +1,182 @@
+// tools/emu/include/hip/hip_runtime.h -- a host-side stand-in for the small
+// part of HIP the engine's kernels use, so the UNMODIFIED kernel sources
+// (noise-cpp_amd/csrc/*.hip, *.hpp) compile as plain C++ and run on the CPU
+// under AddressSanitizer.  Test/debug infrastructure only: it lets a kernel's
+// indexing be checked without risking a GPU memory fault.
+//
+// Execution model: blocks run one after another; a block's threads are real
+// std::threads; each 64-thread wavefront shares an exchange buffer and a
+// barrier, so cross-lane operations (__shfl, __shfl_xor, __ballot,
+// readfirstlane) are exact as long as every lane of the wave reaches them
+// (a divergent cross-lane op deadlocks here -- run under `timeout`).
+// LDS-DMA is a synchronous 16-byte copy; s_waitcnt / fences are no-ops and
+// s_wave_barrier is a real barrier of the wave's threads.
+#pragma once
+#include <atomic>
+#include <barrier>
+#include <cstdint>
+#include <cstring>
+#include <functional>
+#include <thread>
+#include <vector>
+
+#define __global__
+#define __device__
+#define __host__
+#define __forceinline__ inline
+#define __launch_bounds__(...)
+#define __shared__ static
+#define address_space(x) unused  // LDS pointers are plain pointers here
+
+struct uint4 {
+  uint32_t x, y, z, w;
+};
+static inline uint4 make_uint4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
+  return uint4{x, y, z, w};
+}
+
+struct dim3 {
+  unsigned x = 1, y = 1, z = 1;
+  dim3() = default;
+  dim3(unsigned a, unsigned b = 1, unsigned c = 1) : x(a), y(b), z(c) {}
+};
+
+typedef int hipError_t;
+enum {
+  hipSuccess = 0,
+  hipErrorInvalidValue = 1,
+  hipErrorInvalidDevice = 101,
+  hipErrorMemoryAllocation = 2,
+};
+typedef void *hipStream_t;
+
+namespace emu {
+
+struct Wave {
+  std::barrier<> bar{64};
+  uint64_t xch[64];
+};
+
+struct Ctx {
+  dim3 tid, bid;
+  Wave *wave = nullptr;
+  int lane = 0;
+};
+inline thread_local Ctx ctx;
+inline dim3 grid_dim, block_dim;
+
+template <class T>
+inline uint64_t to_bits(T v) {
+  static_assert(sizeof(T) <= 8, "cross-lane value too wide");
+  uint64_t b = 0;
+  std::memcpy(&b, &v, sizeof(T));
+  return b;
+}
+template <class T>
+inline T from_bits(uint64_t b) {
+  T v;
+  std::memcpy(&v, &b, sizeof(T));
+  return v;
+}
+
+template <class T>
+inline T shfl(T v, int src) {
+  Wave &w = *ctx.wave;
+  w.xch[ctx.lane] = to_bits(v);
+  w.bar.arrive_and_wait();
+  const T r = from_bits<T>(w.xch[src & 63]);
+  w.bar.arrive_and_wait();
+  return r;
+}
+
+inline uint64_t ballot(bool p) {
+  Wave &w = *ctx.wave;
+  w.xch[ctx.lane] = p ? 1u : 0u;
+  w.bar.arrive_and_wait();
+  uint64_t m = 0;
+  for (int i = 0; i < 64; ++i) m |= (w.xch[i] & 1u) << i;
+  w.bar.arrive_and_wait();
+  return m;
+}
+
+// run kernel(args...) over the grid: blocks in sequence, threads in parallel
+template <class K, class... A>
+void launch(K kernel, dim3 g, dim3 b, A... args) {
+  grid_dim = g;
+  block_dim = b;
+  const unsigned nt = b.x;
+  const unsigned nw = (nt + 63) / 64;
+  for (unsigned bx = 0; bx < g.x; ++bx) {
+    std::vector<Wave> waves(nw);
+    std::vector<std::thread> th;
+    th.reserve(nt);
+    for (unsigned t = 0; t < nt; ++t) {
+      th.emplace_back([&, t] {
+        ctx.tid = dim3(t);
+        ctx.bid = dim3(bx);
+        ctx.wave = &waves[t / 64];
+        ctx.lane = (int)(t % 64);
+        kernel(args...);
+      });
+    }
+    for (auto &x : th) x.join();
+  }
+}
+
+}  // namespace emu
+
+#define threadIdx (emu::ctx.tid)
+#define blockIdx (emu::ctx.bid)
+#define gridDim (emu::grid_dim)
+#define blockDim (emu::block_dim)
+
+template <class T>
+inline T __shfl(T v, int src, int width = 64) {
+  (void)width;
+  return emu::shfl(v, src);
+}
+template <class T>
+inline T __shfl_xor(T v, int mask, int width = 64) {
+  (void)width;
+  return emu::shfl(v, emu::ctx.lane ^ mask);
+}
+inline uint64_t __ballot(int p) { return emu::ballot(p != 0); }
+
+// returns int, like the real builtin (so sign-extension bugs show here too)
+#define __builtin_amdgcn_readfirstlane(v) ((int)emu::shfl((uint32_t)(v), 0))
+#define __builtin_amdgcn_mbcnt_lo(m, c)                                          \
+  ((uint32_t)(c) + (uint32_t)__builtin_popcount((uint32_t)(m) &                   \
+       (emu::ctx.lane >= 32 ? 0xffffffffu : ((1u << emu::ctx.lane) - 1u))))
+#define __builtin_amdgcn_mbcnt_hi(m, c)                                          \
+  ((uint32_t)(c) + (uint32_t)__builtin_popcount((uint32_t)(m) &                   \
+       (emu::ctx.lane < 32 ? 0u : ((1u << (emu::ctx.lane - 32)) - 1u))))
+#define __builtin_amdgcn_s_waitcnt(x) ((void)0)
+#define __builtin_amdgcn_fence(...) ((void)0)
+// lanes of a real wave run in lockstep; here they meet at every wave_barrier
+// (the kernels put one after each LDS hand-off between lanes)
+#define __builtin_amdgcn_wave_barrier() (emu::ctx.wave->bar.arrive_and_wait())
+#define __builtin_amdgcn_alignbit(hi, lo, s)                                     \
+  ((uint32_t)((((uint64_t)(uint32_t)(hi) << 32) | (uint32_t)(lo)) >> ((s) & 31)))
+// LDS-DMA: lane l copies 16 bytes to lds_base + 16*l
+#define __builtin_amdgcn_global_load_lds(g, l, sz, off, aux)                     \
+  std::memcpy((char *)(void *)(l) + 16 * emu::ctx.lane, (const void *)(g), 16)
+
+inline uint32_t __umul24(uint32_t a, uint32_t b) { return (a & 0xffffffu) * (b & 0xffffffu); }
+inline unsigned long long atomicAdd(unsigned long long *p, unsigned long long v) {
+  return __atomic_fetch_add(p, v, __ATOMIC_SEQ_CST);
+}
+
+#define hipLaunchKernelGGL(kernel, grid, block, shmem, stream, ...)              \
+  emu::launch(kernel, dim3(grid), dim3(block), __VA_ARGS__)
+
+inline hipError_t hipGetLastError() { return hipSuccess; }
+inline hipError_t hipGetDevice(int *d) { *d = 0; return hipSuccess; }
+inline hipError_t hipMalloc(void **p, size_t n) {
+  *p = std::malloc(n);
+  return *p ? hipSuccess : hipErrorMemoryAllocation;
+}
+inline hipError_t hipFree(void *p) { std::free(p); return hipSuccess; }
+inline hipError_t hipMemsetAsync(void *p, int v, size_t n, hipStream_t) {
+  std::memset(p, v, n);
+  return hipSuccess;
+}

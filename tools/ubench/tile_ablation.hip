@@ -29,11 +29,14 @@ int main() {
     printf("%-12s %8.3f ms  %7.1f GB/s alg (2064 B/record)\n", name, ms, R * 2064.0 / (ms * 1e-3) / 1e9);
   };
   const dim3 g(R / 64), b(64);
+  TileArgs ea{}, da{};
+  ea.key = key; ea.in = in; ea.in_stride = L; ea.out = out; ea.out_stride = L + 16; ea.nrec = R;
+  da = ea; da.in = out; da.in_stride = L + 16; da.out = in; da.out_stride = L; da.status = out;
   for (int rep = 0; rep < 2; ++rep) {
-    timeit("full", [&] { hipLaunchKernelGGL((k_aead_tile<false, 1024, true, false, 0>), g, b, 0, 0, key, 0, in, L, out, L + 16, nullptr, R, 0, nullptr, nullptr, nullptr, 0u); });
-    timeit("no_hbm", [&] { hipLaunchKernelGGL((k_aead_tile<false, 1024, true, false, 1>), g, b, 0, 0, key, 0, in, L, out, L + 16, nullptr, R, 0, nullptr, nullptr, nullptr, 0u); });
-    timeit("no_poly", [&] { hipLaunchKernelGGL((k_aead_tile<false, 1024, true, false, 2>), g, b, 0, 0, key, 0, in, L, out, L + 16, nullptr, R, 0, nullptr, nullptr, nullptr, 0u); });
-    timeit("dec_full", [&] { hipLaunchKernelGGL((k_aead_tile<true, 1024, true, false, 0>), g, b, 0, 0, key, 0, out, L + 16, in, L, out, R, 0, nullptr, nullptr, nullptr, 0u); });
+    timeit("full", [&] { hipLaunchKernelGGL((k_aead_tile<false, 1024, true, kTileUniform, 0>), g, b, 0, 0, ea); });
+    timeit("no_hbm", [&] { hipLaunchKernelGGL((k_aead_tile<false, 1024, true, kTileUniform, 1>), g, b, 0, 0, ea); });
+    timeit("no_poly", [&] { hipLaunchKernelGGL((k_aead_tile<false, 1024, true, kTileUniform, 2>), g, b, 0, 0, ea); });
+    timeit("dec_full", [&] { hipLaunchKernelGGL((k_aead_tile<true, 1024, true, kTileUniform, 0>), g, b, 0, 0, da); });
   }
   return 0;
 }

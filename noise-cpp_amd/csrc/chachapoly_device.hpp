@@ -349,6 +349,18 @@ __device__ __forceinline__ void store16(uint8_t *p, uint4 v, int n) {
   if (n > 12) st_bytes(p + 12, v.w, n - 12);
 }
 
+// Keep the first `n` (0..16) bytes of a 16-byte piece, zero the rest (the
+// keystream past a record's end must not reach the MAC).
+__device__ __forceinline__ uint4 mask_bytes(uint4 v, int n) {
+  uint32_t m[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const int b = n - 4 * w;
+    m[w] = b >= 4 ? 0xffffffffu : b <= 0 ? 0u : (1u << (8 * b)) - 1u;
+  }
+  return make_uint4(v.x & m[0], v.y & m[1], v.z & m[2], v.w & m[3]);
+}
+
 // Poly1305 over `n` bytes of associated data, zero padded to 16.
 __device__ __forceinline__ void poly_ad(Poly1305 &p, const uint8_t *ad,
                                         uint32_t n) {

@@ -2,64 +2,62 @@
 // many sessions, mixed sizes (BASELINE config 4, the wavefront load-balance
 // study).
 //
-// A batch of arbitrary records is load-balanced by CLASS, entirely on the
-// device and stream-ordered (no host round trip):
-//   1. k_class_count / k_class_scatter: a counting sort of descriptor
-//      indices by class, wave-aggregated atomics (one atomic per wave and
-//      class);
+// A batch of arbitrary records is load-balanced entirely on the device,
+// stream-ordered (no host round trip):
+//   1. classify (k_cls_count -> k_cls_scan -> k_cls_scatter): a counting
+//      sort of descriptor indices by class with per-wave partial counts and
+//      one scan -- no contended atomics;
 //   2. one launch per class, each reading its slice and count from device
-//      memory (capped grids that stride or pull work, so an empty class
-//      costs one tiny launch):
-//        - tile classes: 16-byte aligned, AD-free records of length
-//          64, 128, 192, 256, 512, 1 Ki, 2 Ki, 4 Ki, 8 Ki, 16 Ki -> the
-//          LDS-staged tile kernel (tile_kernel.hpp, kTileDesc), G lanes per
-//          record;
-//        - wave class: aligned, AD-free, longer than 16 KiB (any length,
-//          e.g. 65519) -> one wavefront per record (wave_kernel.hpp);
-//        - generic: everything else (AD, odd lengths <= 16 KiB, unaligned,
-//          bad key index) -> one lane per record (chachapoly_device.hpp).
-// Small batches (< kClassifyMin records) skip the sort and run the generic
+//      memory:
+//        - tile classes: 16-byte aligned, AD-free records of 64, 128, 192,
+//          256, 512 bytes -> the LDS-staged tile kernel (tile_kernel.hpp,
+//          kTileDesc);
+//        - long records: 16-byte aligned, AD-free, 1024 <= len <= 65535
+//          (any length) -> cut into 1 KiB segments + a tail.  k_seg_prep
+//          derives each record's one-time key and r powers, ONE tile-kernel
+//          launch (kTileSeg) encrypts/decrypts every full segment of every
+//          long record -- uniform 1 KiB work units, whatever the size mix --
+//          and k_seg_finalize combines the segments' Poly1305 partial sums,
+//          runs the tail, the length block and the tag (decrypt: verifies,
+//          and k_seg_fixup restores an in-place record / zeroes a copy whose
+//          tag failed);
+//        - generic: everything else (AD, odd lengths < 1 KiB, unaligned, bad
+//          key index, and long records beyond the segment scratch capacity)
+//          -> one lane per record (chachapoly_device.hpp).
+// Small batches (< kClassifyMin records) skip all this and run the generic
 // kernel directly (latency of single records from CipherState).
-// Scratch (class counts + the sorted index array, 4 B per record) is a
-// grow-only device buffer cached per (device, stream).
+// Scratch is a grow-only device buffer cached per (device, stream).
 #include <mutex>
 #include <vector>
 
 #include "chachapoly_device.hpp"
 #include "launchers.hpp"
 #include "tile_kernel.hpp"
-#include "wave_kernel.hpp"
 
 namespace noise_amd {
 
 constexpr int kGenBlock = 256;
-constexpr int kNumTileCls = 10;
-constexpr int kClsWave = kNumTileCls;
+constexpr int kNumTileCls = 5;            // 64 128 192 256 512
+constexpr int kClsLong = kNumTileCls;     // segmented long records
 constexpr int kClsGeneric = kNumTileCls + 1;
 constexpr int kNumCls = kNumTileCls + 2;
-constexpr uint64_t kClassifyMin = 2048;
-// Grid caps of the per-class launches (capped grids stride / pull work).
-// 2048 single-wave workgroups = 8 per CU, what the register budget keeps
-// resident.  Overridable for the CPU emulation build (tools/emu).
+constexpr int kColSegs = kNumCls;         // classifier column: full segments
+constexpr int kCols = 8;
+#ifndef NOISE_CLASSIFY_MIN  // overridable for the CPU emulation build
+#define NOISE_CLASSIFY_MIN 2048
+#endif
+constexpr uint64_t kClassifyMin = NOISE_CLASSIFY_MIN;
+constexpr uint32_t kLongMax = 65535;      // the Noise message bound
+#ifndef NOISE_SEG_CAP  // overridable for the CPU emulation build (overflow path)
+#define NOISE_SEG_CAP (1ull << 24)
+#endif
+constexpr uint64_t kSegCapMax = NOISE_SEG_CAP;  // 16 Mi segments = 16 GiB per call
+// Grid caps of the per-class launches (capped grids stride over their
+// work).  2048 single-wave workgroups = 8 per CU, what the register and LDS
+// budgets keep resident.  Overridable for the CPU emulation build (tools/emu).
 #ifndef NOISE_GRID_CAP
 #define NOISE_GRID_CAP 2048u
 #endif
-
-__device__ __forceinline__ int tile_class(uint32_t len) {
-  switch (len) {
-    case 64: return 0;
-    case 128: return 1;
-    case 192: return 2;
-    case 256: return 3;
-    case 512: return 4;
-    case 1024: return 5;
-    case 2048: return 6;
-    case 4096: return 7;
-    case 8192: return 8;
-    case 16384: return 9;
-    default: return -1;
-  }
-}
 
 __device__ __forceinline__ int record_class(const noise_gpu_record &d,
                                             uint32_t nkeys, const uint8_t *in,
@@ -68,78 +66,408 @@ __device__ __forceinline__ int record_class(const noise_gpu_record &d,
   if (((reinterpret_cast<uintptr_t>(in + d.in_off) |
         reinterpret_cast<uintptr_t>(out + d.out_off)) & 15u) != 0)
     return kClsGeneric;
-  const int t = tile_class(d.len);
-  if (t >= 0) return t;
-  return d.len > 16384u ? kClsWave : kClsGeneric;
+  switch (d.len) {
+    case 64: return 0;
+    case 128: return 1;
+    case 192: return 2;
+    case 256: return 3;
+    case 512: return 4;
+    default: break;
+  }
+  return (d.len >= 1024u && d.len <= kLongMax) ? kClsLong : kClsGeneric;
 }
 
-// scratch layout (device): counts[kNumCls], cursors[kNumCls], wave cursor,
-// then the sorted index array
-struct RecScratch {
-  unsigned long long counts[kNumCls];
-  unsigned long long cursors[kNumCls];
-  unsigned long long wave_cursor;
-  unsigned long long pad[16 - ((2 * kNumCls + 1) % 16)];
+// device header of the scratch buffer
+struct RecHdr {
+  unsigned long long counts[kCols];    // records per class; [kColSegs] = segments
+  unsigned long long cls_base[kCols];  // start of each class in idx
+  unsigned long long nlong;            // long records handled as segments
+  unsigned long long nseg;             // their full segments
+  unsigned long long pad[14];
 };
-static_assert(sizeof(RecScratch) % 128 == 0, "scratch header alignment");
+static_assert(sizeof(RecHdr) == 256, "scratch header layout");
 
-__global__ __launch_bounds__(kGenBlock) void k_class_count(
-    const noise_gpu_record *__restrict__ recs, uint64_t nrec, uint32_t nkeys,
-    const uint8_t *in, const uint8_t *out, RecScratch *sc) {
-  const uint64_t i = (uint64_t)blockIdx.x * kGenBlock + threadIdx.x;
-  const int cls = i < nrec ? record_class(recs[i], nkeys, in, out) : -1;
-  const uint32_t lane = threadIdx.x & 63u;
+// wave-wide inclusive prefix sum (all 64 lanes participate)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t t = (uint32_t)__shfl((int)v, (int)(lane >= (uint32_t)d ? lane - d : lane));
+    if (lane >= (uint32_t)d) v += t;
+  }
+  return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) v += (uint32_t)__shfl_xor((int)v, d);
+  return v;
+}
+
+// ---- 1. classification ------------------------------------------------------
+// Wave w owns records [w*chunk, (w+1)*chunk).  Per-wave partial counts go
+// to part[w][col]; one wave scans them; the scatter pass writes the sorted
+// index array (class order, record order within a class) and, for long
+// records, their SegRec header fields and the segment list.
+__global__ __launch_bounds__(64) void k_cls_count(
+    const noise_gpu_record *__restrict__ recs, uint64_t nrec, uint32_t chunk,
+    uint32_t nkeys, const uint8_t *in, const uint8_t *out, uint32_t *part) {
+  const uint32_t lane = threadIdx.x;
+  const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
+  const uint64_t e0 = b0 + chunk < nrec ? b0 + chunk : nrec;
+  uint32_t cnt[kNumCls] = {0}, nseg = 0;
 #pragma unroll 1
-  for (int c = 0; c < kNumCls; ++c) {
-    const uint64_t m = __ballot(cls == c);
-    if (m != 0 && lane == (uint32_t)__builtin_ctzll(m))
-      atomicAdd(&sc->counts[c], (unsigned long long)__builtin_popcountll(m));
+  for (uint64_t i0 = b0; i0 < e0; i0 += 64) {
+    const uint64_t i = i0 + lane;
+    int cls = -1;
+    uint32_t nf = 0;
+    if (i < e0) {
+      const noise_gpu_record d = recs[i];
+      cls = record_class(d, nkeys, in, out);
+      nf = cls == kClsLong ? d.len >> 10 : 0u;
+    }
+#pragma unroll
+    for (int c = 0; c < kNumCls; ++c) cnt[c] += (uint32_t)__builtin_popcountll(__ballot(cls == c));
+    nseg += wave_sum(nf);
+  }
+  if (lane < (uint32_t)kCols) {
+    uint32_t v = nseg;
+#pragma unroll
+    for (int c = 0; c < kNumCls; ++c) v = lane == (uint32_t)c ? cnt[c] : v;
+    part[(uint64_t)blockIdx.x * kCols + lane] = v;
   }
 }
 
-__global__ __launch_bounds__(kGenBlock) void k_class_scatter(
-    const noise_gpu_record *__restrict__ recs, uint64_t nrec, uint32_t nkeys,
-    const uint8_t *in, const uint8_t *out, RecScratch *sc, uint32_t *idx) {
-  const uint64_t i = (uint64_t)blockIdx.x * kGenBlock + threadIdx.x;
-  const int cls = i < nrec ? record_class(recs[i], nkeys, in, out) : -1;
-  const uint32_t lane = threadIdx.x & 63u;
-  uint64_t base = 0;
+__global__ __launch_bounds__(64) void k_cls_scan(const uint32_t *part, uint32_t nw,
+                                                 unsigned long long *wbase,
+                                                 RecHdr *hdr, uint64_t segcap) {
+  const uint32_t lane = threadIdx.x;
+  unsigned long long tot[kCols];
 #pragma unroll 1
-  for (int c = 0; c < kNumCls; ++c) {
-    const uint64_t m = __ballot(cls == c);
-    if (m != 0) {
-      const uint32_t leader = (uint32_t)__builtin_ctzll(m);
-      unsigned long long old = 0;
-      if (lane == leader)
-        old = atomicAdd(&sc->cursors[c], (unsigned long long)__builtin_popcountll(m));
-      old = ((unsigned long long)__shfl((int)(uint32_t)(old >> 32), leader) << 32) |
-            (uint32_t)__shfl((int)(uint32_t)old, leader);
+  for (int c = 0; c < kCols; ++c) {
+    unsigned long long run = 0;
+#pragma unroll 1
+    for (uint32_t w0 = 0; w0 < nw; w0 += 64) {
+      const uint32_t w = w0 + lane;
+      const uint32_t v = w < nw ? part[(uint64_t)w * kCols + c] : 0u;
+      const uint32_t inc = wave_incl_scan(v, lane);
+      if (w < nw) wbase[(uint64_t)w * kCols + c] = run + inc - v;
+      run += (uint32_t)__shfl((int)inc, 63);
+    }
+    tot[c] = run;
+  }
+  if (lane == 0) {
+    unsigned long long b = 0;
+    for (int c = 0; c < kCols; ++c) {
+      hdr->counts[c] = tot[c];
+      hdr->cls_base[c] = c < kNumCls ? b : 0ull;
+      if (c < kNumCls) b += tot[c];
+    }
+    // lowered by k_cls_scatter if the segment scratch overflows
+    hdr->nlong = tot[kClsLong];
+    hdr->nseg = tot[kColSegs] < segcap ? tot[kColSegs] : segcap;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_cls_scatter(
+    const noise_gpu_record *__restrict__ recs, uint64_t nrec, uint32_t chunk,
+    uint32_t nkeys, const uint8_t *in, const uint8_t *out,
+    const unsigned long long *wbase, RecHdr *hdr, uint32_t *idx, SegRec *rt,
+    SegEntry *segs, uint64_t segcap) {
+  const uint32_t lane = threadIdx.x;
+  const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
+  const uint64_t e0 = b0 + chunk < nrec ? b0 + chunk : nrec;
+  unsigned long long run[kCols];
+#pragma unroll
+  for (int c = 0; c < kCols; ++c) run[c] = wbase[(uint64_t)blockIdx.x * kCols + c];
+  unsigned long long cbase[kNumCls];
+#pragma unroll
+  for (int c = 0; c < kNumCls; ++c) cbase[c] = hdr->cls_base[c];
+  bool overflow = false;
+  unsigned long long ov_q = ~0ull, ov_seg = ~0ull;
+#pragma unroll 1
+  for (uint64_t i0 = b0; i0 < e0; i0 += 64) {
+    const uint64_t i = i0 + lane;
+    int cls = -1;
+    noise_gpu_record d{};
+    if (i < e0) {
+      d = recs[i];
+      cls = record_class(d, nkeys, in, out);
+    }
+    const uint32_t nf = cls == kClsLong ? d.len >> 10 : 0u;
+    unsigned long long q = 0;
+#pragma unroll
+    for (int c = 0; c < kNumCls; ++c) {
+      const uint64_t m = __ballot(cls == c);
       if (cls == c) {
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
             (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        idx[base + old + rank] = (uint32_t)i;
+        q = run[c] + rank;
+        idx[cbase[c] + q] = (uint32_t)i;
+      }
+      run[c] += (unsigned long long)__builtin_popcountll(m);
+    }
+    // long records: header fields of their SegRec, first segment index
+    const uint32_t inc = wave_incl_scan(nf, lane);
+    const uint32_t total = (uint32_t)__shfl((int)inc, 63);
+    const uint32_t rel0 = inc - nf;
+    if (cls == kClsLong) {
+      const unsigned long long seg0 = run[kColSegs] + rel0;
+      SegRec &R = rt[q];
+      R.in_off = d.in_off;
+      R.out_off = d.out_off;
+      R.nonce = d.nonce;
+      R.seg0 = seg0;
+      R.key_idx = d.key_idx;
+      R.di = (uint32_t)i;
+      R.len = d.len;
+      R.nfull = nf;
+      if (seg0 + nf > segcap) {  // beyond the scratch: this and later long records go generic
+        overflow = true;
+        ov_q = q < ov_q ? q : ov_q;
+        ov_seg = seg0 < ov_seg ? seg0 : ov_seg;
       }
     }
-    base += sc->counts[c];
+    // segment list entries (q, s), written cooperatively: entry k of this
+    // group belongs to the first lane whose inclusive count exceeds k
+#pragma unroll 1
+    for (uint32_t k0 = 0; k0 < total; k0 += 64) {
+      const uint32_t k = k0 + lane;
+      uint32_t lo = 0;
+#pragma unroll
+      for (int step = 32; step >= 1; step >>= 1) {
+        const uint32_t probe = (uint32_t)__shfl((int)inc, (int)(lo + step - 1));
+        if (probe <= k) lo += step;
+      }
+      const uint32_t oq = (uint32_t)__shfl((int)(uint32_t)q, (int)lo);
+      const uint32_t orel = (uint32_t)__shfl((int)rel0, (int)lo);
+      const unsigned long long pos = run[kColSegs] + k;
+      if (k < total && pos < segcap) segs[pos] = SegEntry{oq, k - orel};
+    }
+    run[kColSegs] += total;
+  }
+  if (overflow) {  // rare: only when the long records exceed kSegCapMax segments
+    atomicMin(&hdr->nlong, ov_q);
+    atomicMin(&hdr->nseg, ov_seg);
   }
 }
 
-// one lane per record; idx == nullptr: record i directly (small batches)
+// ---- 2. long records --------------------------------------------------------
+// k_seg_prep: lane per long record -> ChaCha block 0 (one-time key r, s),
+// r^16, r^32 (the segment kernel's 4-lane recombination) and r^64 (the
+// finalize kernel's Horner step over segments).
+__global__ __launch_bounds__(64) void k_seg_prep(const uint8_t *__restrict__ keys,
+                                                 SegRec *rt, const RecHdr *hdr) {
+  const uint64_t n = hdr->nlong;
+#pragma unroll 1
+  for (uint64_t q = (uint64_t)blockIdx.x * 64 + threadIdx.x; q < n;
+       q += (uint64_t)gridDim.x * 64) {
+    SegRec &R = rt[q];
+    const u32x4 *kp = reinterpret_cast<const u32x4 *>(keys + 32ull * R.key_idx);
+    const u32x4 ka = kp[0], kb = kp[1];
+    const uint32_t k[8] = {ka.x, ka.y, ka.z, ka.w, kb.x, kb.y, kb.z, kb.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) R.k[i] = k[i];
+    uint32_t otk[16];
+    chacha20_block(k, 0u, (uint32_t)R.nonce, (uint32_t)(R.nonce >> 32), otk);
+    const uint32_t r0 = otk[0] & 0x0fffffffu, r1 = otk[1] & 0x0ffffffcu,
+                   r2 = otk[2] & 0x0ffffffcu, r3 = otk[3] & 0x0ffffffcu;
+    R.r[0] = r0; R.r[1] = r1; R.r[2] = r2; R.r[3] = r3;
+    R.s[0] = otk[4]; R.s[1] = otk[5]; R.s[2] = otk[6]; R.s[3] = otk[7];
+    F26 x = to26(r0, r1, r2, r3, 0u);
+    x = mul26(x, x);  // r^2
+    x = mul26(x, x);  // r^4
+    x = mul26(x, x);  // r^8
+    x = mul26(x, x);  // r^16
+    const F26 x32 = mul26(x, x), x64 = mul26(x32, x32);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      R.pw16[i] = x.a[i];
+      R.pw32[i] = x32.a[i];
+      R.r64[i] = x64.a[i];
+    }
+  }
+}
+
+// k_seg_finalize: lane per long record.  h = Horner over the segments'
+// partial sums in R = r^64, then the tail (len % 1024 bytes, ChaCha counters
+// from 1 + 16 nfull) lane-serially, the length block and the tag.  Decrypt
+// verifies the tag first (MAC over the tail ciphertext), decrypts the tail
+// only if it matches, and writes the record's status.
+template <bool DECRYPT>
+__global__ __launch_bounds__(64) void k_seg_finalize(
+    const uint8_t *__restrict__ keys, const SegRec *__restrict__ rt,
+    const SegPartial *__restrict__ partial, const RecHdr *hdr,
+    const uint8_t *in, uint8_t *out, uint8_t *status) {
+  const uint64_t n = hdr->nlong;
+#pragma unroll 1
+  for (uint64_t q = (uint64_t)blockIdx.x * 64 + threadIdx.x; q < n;
+       q += (uint64_t)gridDim.x * 64) {
+    const SegRec &R = rt[q];
+    F26 R64, acc;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) R64.a[i] = R.r64[i];
+    const uint32_t nf = R.nfull;
+    {
+      const SegPartial &P0 = partial[R.seg0];
+      acc = to26(P0.h[0], P0.h[1], P0.h[2], P0.h[3], P0.h[4]);
+    }
+#pragma unroll 1
+    for (uint32_t s = 1; s < nf; ++s) {
+      const SegPartial &P = partial[R.seg0 + s];
+      acc = mul26(acc, R64);
+      const F26 t = to26(P.h[0], P.h[1], P.h[2], P.h[3], P.h[4]);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) acc.a[i] += t.a[i];
+      carry26(acc);
+    }
+    carry26(acc);
+    Poly1305 p;
+    from26(acc, p.h0, p.h1, p.h2, p.h3, p.h4);
+    p.r0 = R.r[0]; p.r1 = R.r[1]; p.r2 = R.r[2]; p.r3 = R.r[3];
+    p.rr0 = (p.r0 >> 2) * 5u;
+    p.rr1 = p.r1 + (p.r1 >> 2);
+    p.rr2 = p.r2 + (p.r2 >> 2);
+    p.rr3 = p.r3 + (p.r3 >> 2);
+    p.r0lo = p.r0 & 3u;
+    p.s0 = R.s[0]; p.s1 = R.s[1]; p.s2 = R.s[2]; p.s3 = R.s[3];
+
+    uint32_t k[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) k[i] = R.k[i];
+    const uint32_t n_lo = (uint32_t)R.nonce, n_hi = (uint32_t)(R.nonce >> 32);
+    const uint32_t len = R.len, tb = len - 1024u * nf;
+    const uint8_t *src = in + R.in_off + 1024ull * nf;
+    uint8_t *dst = out + R.out_off + 1024ull * nf;
+    const uint32_t cb = 1u + 16u * nf;
+
+    if (!DECRYPT) {
+#pragma unroll 1
+      for (uint32_t off = 0; off < tb; off += 64) {
+        uint32_t ks[16];
+        chacha20_block(k, cb + (off >> 6), n_lo, n_hi, ks);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const int m = (int)(tb - off) - 16 * w;
+          if (m <= 0) break;
+          const int nb = m >= 16 ? 16 : m;
+          const uint4 v = nb == 16 ? load16<true>(src + off + 16 * w, 16)
+                                   : load16<false>(src + off + 16 * w, nb);
+          const uint4 o = mask_bytes(make_uint4(v.x ^ ks[4 * w], v.y ^ ks[4 * w + 1],
+                                                v.z ^ ks[4 * w + 2], v.w ^ ks[4 * w + 3]), nb);
+          poly_block(p, o.x, o.y, o.z, o.w);
+          if (nb == 16) store16<true>(dst + off + 16 * w, o, 16);
+          else store16<false>(dst + off + 16 * w, o, nb);
+        }
+      }
+      poly_block(p, 0u, 0u, len, 0u);  // LE64(ad_len = 0) || LE64(len)
+      uint32_t tag[4];
+      poly_final(p, tag);
+      uint8_t *tp = out + R.out_off + len;
+      if ((len & 15u) == 0) store16<true>(tp, make_uint4(tag[0], tag[1], tag[2], tag[3]), 16);
+      else store16<false>(tp, make_uint4(tag[0], tag[1], tag[2], tag[3]), 16);
+    } else {
+      // MAC over the tail ciphertext, then the length block and the tag
+#pragma unroll 1
+      for (uint32_t off = 0; off < tb; off += 16) {
+        const uint32_t nb = tb - off >= 16 ? 16u : tb - off;
+        const uint4 v = nb == 16 ? load16<true>(src + off, 16) : load16<false>(src + off, (int)nb);
+        poly_block(p, v.x, v.y, v.z, v.w);
+      }
+      poly_block(p, 0u, 0u, len, 0u);
+      uint32_t tag[4];
+      poly_final(p, tag);
+      const uint8_t *tp = in + R.in_off + len;
+      const uint4 want = (len & 15u) == 0 ? load16<true>(tp, 16) : load16<false>(tp, 16);
+      const uint32_t diff = (want.x ^ tag[0]) | (want.y ^ tag[1]) | (want.z ^ tag[2]) |
+                            (want.w ^ tag[3]);
+      const bool ok = diff == 0u;
+      const bool in_place = src == dst;
+      if (ok || !in_place) {
+#pragma unroll 1
+        for (uint32_t off = 0; off < tb; off += 64) {
+          uint32_t ks[16];
+          if (ok) chacha20_block(k, cb + (off >> 6), n_lo, n_hi, ks);
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const int m = (int)(tb - off) - 16 * w;
+            if (m <= 0) break;
+            const int nb = m >= 16 ? 16 : m;
+            uint4 o = make_uint4(0u, 0u, 0u, 0u);  // failed copy: zeroed
+            if (ok) {
+              const uint4 v = nb == 16 ? load16<true>(src + off + 16 * w, 16)
+                                       : load16<false>(src + off + 16 * w, nb);
+              o = make_uint4(v.x ^ ks[4 * w], v.y ^ ks[4 * w + 1], v.z ^ ks[4 * w + 2],
+                             v.w ^ ks[4 * w + 3]);
+            }
+            if (nb == 16) store16<true>(dst + off + 16 * w, o, 16);
+            else store16<false>(dst + off + 16 * w, o, nb);
+          }
+        }
+      }
+      status[R.di] = ok ? NOISE_GPU_REC_OK : NOISE_GPU_REC_BAD_MAC;
+    }
+  }
+}
+
+// k_seg_fixup (decrypt): lane per full segment.  The segment kernel wrote
+// plaintext before the tag was known; for a record whose tag failed, put
+// the ciphertext back (in place: XOR the keystream again, leaving the buffer
+// as it was -- crypto_aead_read semantics) or zero the copy.
+__global__ __launch_bounds__(64) void k_seg_fixup(
+    const uint8_t *__restrict__ keys, const SegEntry *__restrict__ segs,
+    const SegRec *__restrict__ rt, const RecHdr *hdr, const uint8_t *in,
+    uint8_t *out, const uint8_t *status) {
+  const uint64_t n = hdr->nseg;
+#pragma unroll 1
+  for (uint64_t g = (uint64_t)blockIdx.x * 64 + threadIdx.x; g < n;
+       g += (uint64_t)gridDim.x * 64) {
+    const SegEntry e = segs[g];
+    const SegRec &R = rt[e.q];
+    if (status[R.di] == NOISE_GPU_REC_OK) continue;
+    uint8_t *dst = out + R.out_off + 1024ull * e.s;
+    const bool in_place = in + R.in_off == out + R.out_off;
+    uint32_t k[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) k[i] = R.k[i];
+#pragma unroll 1
+    for (uint32_t c = 0; c < 16; ++c) {
+      uint32_t ks[16];
+      if (in_place)
+        chacha20_block(k, 1u + 16u * e.s + c, (uint32_t)R.nonce, (uint32_t)(R.nonce >> 32), ks);
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        uint4 o = make_uint4(0u, 0u, 0u, 0u);
+        if (in_place) {
+          const uint4 v = load16<true>(dst + 64u * c + 16 * w, 16);
+          o = make_uint4(v.x ^ ks[4 * w], v.y ^ ks[4 * w + 1], v.z ^ ks[4 * w + 2],
+                         v.w ^ ks[4 * w + 3]);
+        }
+        store16<true>(dst + 64u * c + 16 * w, o, 16);
+      }
+    }
+  }
+}
+
+// ---- generic: one lane per record ------------------------------------------
+// idx == nullptr: record i directly (small batches).  Otherwise the generic
+// class, followed by the long records the segment scratch could not take.
 template <bool DECRYPT>
 __global__ __launch_bounds__(kGenBlock) void k_aead_records(
     const uint8_t *__restrict__ keys, uint32_t nkeys,
     const noise_gpu_record *__restrict__ recs, uint64_t nrec,
-    const uint32_t *__restrict__ idx, const unsigned long long *counts,
+    const uint32_t *__restrict__ idx, const RecHdr *hdr,
     const uint8_t *in, uint8_t *out, const uint8_t *ad, uint8_t *status) {
-  uint64_t base = 0, n = nrec;
+  uint64_t base = 0, n = nrec, base2 = 0, n2 = 0;
   if (idx) {
-    for (int c = 0; c < kClsGeneric; ++c) base += counts[c];
-    n = counts[kClsGeneric];
+    base = hdr->cls_base[kClsGeneric];
+    n = hdr->counts[kClsGeneric];
+    base2 = hdr->cls_base[kClsLong] + hdr->nlong;
+    n2 = hdr->counts[kClsLong] - hdr->nlong;
   }
 #pragma unroll 1
-  for (uint64_t i = (uint64_t)blockIdx.x * kGenBlock + threadIdx.x; i < n;
+  for (uint64_t i = (uint64_t)blockIdx.x * kGenBlock + threadIdx.x; i < n + n2;
        i += (uint64_t)gridDim.x * kGenBlock) {
-    const uint64_t di = idx ? idx[base + i] : i;
+    const uint64_t di = idx ? idx[i < n ? base + i : base2 + (i - n)] : i;
     const noise_gpu_record r = recs[di];
     if (r.key_idx >= nkeys) {  // never index outside the key table
       if (DECRYPT) status[di] = NOISE_GPU_REC_BAD_KEY;
@@ -197,29 +525,37 @@ static hipError_t scratch_get(void **p, size_t bytes, hipStream_t stream) {
   return hipSuccess;
 }
 
+static inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+static inline unsigned capped(uint64_t want, uint64_t cap) {
+  if (want == 0) want = 1;
+  return (unsigned)(want < cap ? want : cap);
+}
+
 template <bool DECRYPT>
-static void launch_desc_tiles(const TileArgs &ta, uint64_t nrec, hipStream_t stream) {
+static void launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr *hdr,
+                           const uint8_t *keys, uint64_t segbound, const uint8_t *in,
+                           uint8_t *out, uint8_t *status, hipStream_t stream) {
   const dim3 bt(64);
-  auto grid = [&](int rpt_super) {
-    (void)rpt_super;
-    const uint64_t want = (nrec + 63) / 64;
-    return dim3((unsigned)(want < NOISE_GRID_CAP ? want : NOISE_GRID_CAP));
-  };
+  const dim3 grid(capped((nrec + 63) / 64, NOISE_GRID_CAP));
   TileArgs a = ta;
 #define NOISE_DESC_TILE(C, LEN)                                                \
   a.cls = C;                                                                   \
-  hipLaunchKernelGGL((k_aead_tile<DECRYPT, LEN, false, kTileDesc>), grid(LEN), bt, 0, stream, a);
+  hipLaunchKernelGGL((k_aead_tile<DECRYPT, LEN, false, kTileDesc>), grid, bt, 0, stream, a);
   NOISE_DESC_TILE(0, 64)
   NOISE_DESC_TILE(1, 128)
   NOISE_DESC_TILE(2, 192)
   NOISE_DESC_TILE(3, 256)
   NOISE_DESC_TILE(4, 512)
-  NOISE_DESC_TILE(5, 1024)
-  NOISE_DESC_TILE(6, 2048)
-  NOISE_DESC_TILE(7, 4096)
-  NOISE_DESC_TILE(8, 8192)
-  NOISE_DESC_TILE(9, 16384)
 #undef NOISE_DESC_TILE
+  // long records: prep -> every full segment in one tile launch -> finalize
+  hipLaunchKernelGGL(k_seg_prep, grid, bt, 0, stream, keys, const_cast<SegRec *>(ta.rt), hdr);
+  const dim3 gseg(capped((segbound + 63) / 64, NOISE_GRID_CAP));
+  hipLaunchKernelGGL((k_aead_tile<DECRYPT, 1024, false, kTileSeg>), gseg, bt, 0, stream, a);
+  hipLaunchKernelGGL((k_seg_finalize<DECRYPT>), grid, bt, 0, stream, keys, ta.rt, ta.partial,
+                     hdr, in, out, status);
+  if (DECRYPT)
+    hipLaunchKernelGGL(k_seg_fixup, gseg, bt, 0, stream, keys, ta.segs, ta.rt, hdr, in, out,
+                       status);
 }
 
 hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
@@ -239,15 +575,37 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   }
   if (nrec > 0xffffffffull) return hipErrorInvalidValue;  // 32-bit indices
 
+  // classifier geometry: at most 2048 waves of >= 512 records
+  uint64_t chunk = align_up((nrec + 2047) / 2048, 64);
+  if (chunk < 512) chunk = 512;
+  const uint64_t nw = (nrec + chunk - 1) / chunk;
+  const uint64_t segcap = nrec * 63 < kSegCapMax ? nrec * 63 : kSegCapMax;
+
+  // scratch: header | part[nw][8] | wbase[nw][8] | idx[nrec] | rt[nrec] |
+  //          segs[segcap] | partial[segcap]
+  const uint64_t o_part = sizeof(RecHdr);
+  const uint64_t o_wbase = align_up(o_part + nw * kCols * 4, 256);
+  const uint64_t o_idx = align_up(o_wbase + nw * kCols * 8, 256);
+  const uint64_t o_rt = align_up(o_idx + nrec * 4, 256);
+  const uint64_t o_segs = align_up(o_rt + nrec * sizeof(SegRec), 256);
+  const uint64_t o_part2 = align_up(o_segs + segcap * sizeof(SegEntry), 256);
+  const uint64_t bytes = o_part2 + segcap * sizeof(SegPartial);
   void *mem = nullptr;
-  hipError_t e = scratch_get(&mem, sizeof(RecScratch) + 4 * nrec, stream);
+  hipError_t e = scratch_get(&mem, bytes, stream);
   if (e != hipSuccess) return e;
-  RecScratch *sc = static_cast<RecScratch *>(mem);
-  uint32_t *idx = reinterpret_cast<uint32_t *>(sc + 1);
-  e = hipMemsetAsync(sc, 0, sizeof(RecScratch), stream);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_class_count, dim3((unsigned)gblocks), bg, 0, stream, recs, nrec, nkeys, in, out, sc);
-  hipLaunchKernelGGL(k_class_scatter, dim3((unsigned)gblocks), bg, 0, stream, recs, nrec, nkeys, in, out, sc, idx);
+  uint8_t *base = static_cast<uint8_t *>(mem);
+  RecHdr *hdr = reinterpret_cast<RecHdr *>(base);
+  uint32_t *part = reinterpret_cast<uint32_t *>(base + o_part);
+  unsigned long long *wbase = reinterpret_cast<unsigned long long *>(base + o_wbase);
+  uint32_t *idx = reinterpret_cast<uint32_t *>(base + o_idx);
+  SegRec *rt = reinterpret_cast<SegRec *>(base + o_rt);
+  SegEntry *segs = reinterpret_cast<SegEntry *>(base + o_segs);
+  SegPartial *partial = reinterpret_cast<SegPartial *>(base + o_part2);
+
+  const dim3 b64(64);
+  hipLaunchKernelGGL(k_cls_count, dim3((unsigned)nw), b64, 0, stream, recs, nrec, (uint32_t)chunk, nkeys, in, out, part);
+  hipLaunchKernelGGL(k_cls_scan, dim3(1), b64, 0, stream, part, (uint32_t)nw, wbase, hdr, segcap);
+  hipLaunchKernelGGL(k_cls_scatter, dim3((unsigned)nw), b64, 0, stream, recs, nrec, (uint32_t)chunk, nkeys, in, out, wbase, hdr, idx, rt, segs, segcap);
 
   TileArgs ta{};
   ta.in = in;
@@ -257,22 +615,20 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   ta.nkeys = nkeys;
   ta.recs = recs;
   ta.idx = idx;
-  ta.counts = sc->counts;
-  if (decrypt) launch_desc_tiles<true>(ta, nrec, stream);
-  else launch_desc_tiles<false>(ta, nrec, stream);
-
-  const uint64_t wblocks = (nrec + kWaveBatch - 1) / kWaveBatch;
-  const dim3 gw((unsigned)(wblocks < NOISE_GRID_CAP ? wblocks : NOISE_GRID_CAP)), bw(64);
-  if (decrypt)
-    hipLaunchKernelGGL((k_aead_wave<true>), gw, bw, 0, stream, keys, nkeys, recs, idx, sc->counts, kClsWave, &sc->wave_cursor, in, out, status);
-  else
-    hipLaunchKernelGGL((k_aead_wave<false>), gw, bw, 0, stream, keys, nkeys, recs, idx, sc->counts, kClsWave, &sc->wave_cursor, in, out, status);
+  ta.cls_base = hdr->cls_base;
+  ta.counts = hdr->counts;
+  ta.segs = segs;
+  ta.rt = rt;
+  ta.partial = partial;
+  ta.nseg = &hdr->nseg;
+  if (decrypt) launch_classes<true>(ta, nrec, hdr, keys, segcap, in, out, status, stream);
+  else launch_classes<false>(ta, nrec, hdr, keys, segcap, in, out, status, stream);
 
   const dim3 gg((unsigned)(gblocks < 2 * NOISE_GRID_CAP ? gblocks : 2 * NOISE_GRID_CAP));
   if (decrypt)
-    hipLaunchKernelGGL((k_aead_records<true>), gg, bg, 0, stream, keys, nkeys, recs, nrec, idx, sc->counts, in, out, ad, status);
+    hipLaunchKernelGGL((k_aead_records<true>), gg, bg, 0, stream, keys, nkeys, recs, nrec, idx, hdr, in, out, ad, status);
   else
-    hipLaunchKernelGGL((k_aead_records<false>), gg, bg, 0, stream, keys, nkeys, recs, nrec, idx, sc->counts, in, out, ad, status);
+    hipLaunchKernelGGL((k_aead_records<false>), gg, bg, 0, stream, keys, nkeys, recs, nrec, idx, hdr, in, out, ad, status);
   return hipGetLastError();
 }
 

@@ -69,6 +69,35 @@ enum TileMode : int {
   kTileUniform = 0,   // one key, nonce0 + i, record i at in + i*in_stride
   kTileSessions = 1,  // key row keys[key_idx[i]], nonce nonces[i], strided
   kTileDesc = 2,      // descriptor recs[idx[base + i]] (records API class)
+  kTileSeg = 3,       // 1 KiB segment g of a long record (segs[g] -> SegRec):
+                      // ciphertext + Poly1305 partial sum, no tag
+};
+
+// ---- long records as 1 KiB segments (records_kernels.hip) -----------------
+// A record of len >= 1024 bytes is cut into nfull = len / 1024 full segments
+// plus a tail of len % 1024 bytes.  Segment s covers bytes [1024 s, 1024 s +
+// 1024): ChaCha blocks 1 + 16 s .. 16 + 16 s and Poly1305 blocks 64 s ..
+// 64 s + 63.  The tile kernel (kTileSeg) encrypts/decrypts every full
+// segment of every long record as if it were a 1 KiB record -- one uniform,
+// load-balanced launch -- and leaves the segment's Poly1305 Horner sum
+//   P_s = sum_{i<64} m_{64s+i} r^(64-i)
+// in SegPartial.  The finalize kernel combines h = sum_s P_s r^(64(nfull-1-s))
+// (Horner in R = r^64), runs the tail, the length block and the tag.
+struct SegRec {                  // one per long record, 176 B
+  uint64_t in_off, out_off, nonce, seg0;  // seg0: index of segment 0
+  uint32_t k[8];                 // the record's key (copied from the key table)
+  uint32_t key_idx, di, len, nfull;       // di: descriptor index
+  uint32_t r[4];                 // clamped Poly1305 r (radix 2^32)
+  uint32_t s[4];                 // Poly1305 s
+  uint32_t pw16[5], pw32[5], r64[5];      // r^16, r^32, r^64 (radix 2^26)
+  uint32_t pad;
+};
+static_assert(sizeof(SegRec) == 176, "SegRec layout");
+struct SegEntry {                // one per full segment
+  uint32_t q, s;                 // long-record index, segment number
+};
+struct SegPartial {              // P_s in radix 2^32 (h4 small)
+  uint32_t h[8];
 };
 
 struct TileArgs {
@@ -87,15 +116,26 @@ struct TileArgs {
   const uint64_t *nonces;   // kTileSessions
   const noise_gpu_record *recs;  // kTileDesc
   const uint32_t *idx;           // kTileDesc: class-sorted descriptor indices
-  const unsigned long long *counts;  // kTileDesc: per-class counts (device)
+  const unsigned long long *cls_base;  // kTileDesc: class start in idx (device)
+  const unsigned long long *counts;    // kTileDesc: per-class counts (device)
   int cls;                       // kTileDesc: this launch's class
+  const SegEntry *segs;          // kTileSeg
+  const SegRec *rt;              // kTileSeg
+  SegPartial *partial;           // kTileSeg
+  const unsigned long long *nseg;  // kTileSeg: number of segments (device)
 };
 
-// kTileDesc: the class's slice of the sorted index array
+// kTileDesc: the class's slice of the sorted index array; kTileSeg: all
+// segments
+template <int MODE>
 __device__ __forceinline__ void desc_class_range(const TileArgs &a,
                                                  uint64_t &base, uint64_t &n) {
   base = 0;
-  for (int c = 0; c < a.cls; ++c) base += a.counts[c];
+  if (MODE == kTileSeg) {
+    n = *a.nseg;
+    return;
+  }
+  base = a.cls_base[a.cls];
   n = a.counts[a.cls];
 }
 
@@ -108,7 +148,8 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
                                           uint32_t own_in_hi) {
   using C = TileCfg<L>;
   if (ABL == 1) return;
-  constexpr int IN_SLOTS = DECRYPT ? C::NSLOT : C::REC_SLOTS;
+  constexpr bool TAGGED_IN = DECRYPT && MODE != kTileSeg;  // ct || tag pieces
+  constexpr int IN_SLOTS = TAGGED_IN ? C::NSLOT : C::REC_SLOTS;
   if (CONTIG) {
     // slot s = 64q + lane holds piece swz(s) = 64q + gl[q & 3]; packed
     // records put piece g of an encrypt tile at byte 16g and of a decrypt
@@ -124,7 +165,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
             (const void *)(base + off),
             (__attribute__((address_space(3))) void *)(lds3 + 64 * q), 16, 0, 0);
     }
-    if (DECRYPT) {  // tag pieces: slot REC_SLOTS + r <- piece (r, SPR)
+    if (TAGGED_IN) {  // tag pieces: slot REC_SLOTS + r <- piece (r, SPR)
 #pragma unroll
       for (int q = C::REC_SLOTS / 64; q < (C::NSLOT + 63) / 64; ++q) {
         const uint32_t r = 64u * q + lane - C::REC_SLOTS;
@@ -132,6 +173,21 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
           __builtin_amdgcn_global_load_lds(
               (const void *)(base + 16u * (r * (C::SPR + 1) + C::SPR)),
               (__attribute__((address_space(3))) void *)(lds3 + 64 * q), 16, 0, 0);
+      }
+    }
+  } else if (MODE == kTileSeg) {
+    // 1 KiB segments: DMA instruction q moves all 64 pieces of segment q, so
+    // its offset is wave-uniform -- read from the segment's key lane
+    // (v_readlane into SGPRs) instead of a per-lane shuffle
+#pragma unroll
+    for (int q = 0; q < C::RPT; ++q) {
+      if ((uint32_t)q < nv) {
+        const uint32_t kl = t_rpt + q;
+        const uint64_t off = join64((uint32_t)__builtin_amdgcn_readlane((int)own_in_hi, (int)kl),
+                                    (uint32_t)__builtin_amdgcn_readlane((int)own_in_lo, (int)kl));
+        __builtin_amdgcn_global_load_lds(
+            (const void *)(in + off + 16u * gl[q & 3]),
+            (__attribute__((address_space(3))) void *)(lds3 + 64 * q), 16, 0, 0);
       }
     }
   } else {
@@ -148,7 +204,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
         p = C::SPR;
       }
       const uint8_t *rec_base;
-      if (MODE == kTileDesc) {  // record r's offset lives in key lane t*RPT + r
+      if (MODE == kTileDesc || MODE == kTileSeg) {  // offset of record r: key lane t*RPT + r
         const uint32_t src = t_rpt + (r < (uint32_t)C::RPT ? r : 0u);
         const uint64_t off = ((uint64_t)(uint32_t)__shfl((int)own_in_hi, src) << 32) |
                              (uint32_t)__shfl((int)own_in_lo, src);
@@ -170,22 +226,29 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
 // takes per-record offsets from the descriptor (16-byte aligned; the
 // classifier guarantees it) and is launched with a capped grid that strides
 // over the class's super-tiles.
+// kTileSeg (L = 1024): unit i is full segment i of a long record (SegEntry ->
+// SegRec): no key block (r and its powers come from the SegRec), ChaCha
+// counters 1 + 16 s + ..., no tag: the segment's Poly1305 partial sum goes to
+// a.partial[i].  Decrypt writes the plaintext unconditionally (the finalize
+// and fix-up kernels restore or zero the record if its tag fails).
 // ABL (ablation, tools/ubench only; the product uses 0): 1 = no HBM traffic
 // (compute on whatever the LDS holds), 2 = no Poly1305 work.
 template <bool DECRYPT, int L, bool CONTIG, int MODE = kTileUniform, int ABL = 0>
 __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
   using C = TileCfg<L>;
   constexpr bool KEYED = MODE != kTileUniform;
-  constexpr int OPR = DECRYPT ? C::SPR : C::SPR + 1;  // out pieces / record
+  constexpr bool SEG = MODE == kTileSeg;
+  constexpr int OPR = (DECRYPT || SEG) ? C::SPR : C::SPR + 1;  // out pieces / record
   constexpr int OUT_SLOTS = C::RPT * OPR;
   constexpr int NOUT = (OUT_SLOTS + 63) / 64;          // store instructions
-  static_assert(!(CONTIG && MODE == kTileDesc), "descriptor tiles are strided");
+  static_assert(!(CONTIG && (MODE == kTileDesc || SEG)), "descriptor tiles are strided");
+  static_assert(!SEG || L == 1024, "segments are 1 KiB");
   __shared__ uint4 lds[C::NSLOT];
   const uint32_t lane = threadIdx.x;
   const uint8_t *in = a.in;
   uint8_t *out = a.out;
   uint64_t nrec = a.nrec, dbase = 0;
-  if (MODE == kTileDesc) desc_class_range(a, dbase, nrec);
+  if (MODE == kTileDesc || SEG) desc_class_range<MODE>(a, dbase, nrec);
   uint32_t k[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) k[i] = a.key.w[i];
@@ -204,8 +267,42 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
   F26 pw[C::LOG2G > 0 ? C::LOG2G : 1];
   uint32_t own_k[8], own_nlo = 0, own_nhi = 0;  // keyed modes: this lane's record
   uint32_t own_in_lo = 0, own_in_hi = 0, own_out_lo = 0, own_out_hi = 0, own_di = 0;
+  uint32_t own_cb = 0;  // kTileSeg: first ChaCha block counter - 1 (16 s)
   bool own_bad = false, own_inplace = false;
-  {
+  if (SEG) {
+    const uint64_t g = super0 + lane;
+    uint64_t n = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) own_k[i] = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) kr[i] = kss[i] = 0u;
+#pragma unroll
+    for (int b = 0; b < (C::LOG2G > 0 ? C::LOG2G : 1); ++b)
+#pragma unroll
+      for (int i = 0; i < 5; ++i) pw[b].a[i] = i == 0 ? 1u : 0u;
+    if (g < nrec) {
+      const SegEntry e = a.segs[g];
+      const SegRec &R = a.rt[e.q];
+      n = R.nonce;
+      const uint64_t io = R.in_off + 1024ull * e.s, oo = R.out_off + 1024ull * e.s;
+      own_in_lo = (uint32_t)io; own_in_hi = (uint32_t)(io >> 32);
+      own_out_lo = (uint32_t)oo; own_out_hi = (uint32_t)(oo >> 32);
+      own_cb = 16u * e.s;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) own_k[i] = R.k[i];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { kr[i] = R.r[i]; kss[i] = 0u; }
+#pragma unroll
+      for (int i = 0; i < 5; ++i) { pw[0].a[i] = R.pw16[i]; pw[C::LOG2G > 1 ? 1 : 0].a[i] = R.pw32[i]; }
+    }
+    own_nlo = (uint32_t)n;
+    own_nhi = (uint32_t)(n >> 32);
+    const uint64_t left = nrec - super0;
+    tile_load<L, DECRYPT, CONTIG, MODE, ABL>(
+        NOISE_LDS3(lds), in, a.in_stride, super0,
+        left < (uint64_t)C::RPT ? (uint32_t)left : C::RPT, lane, gl, 0u,
+        own_in_lo, own_in_hi);
+  } else {
     uint64_t n = a.nonce0 + super0 + lane;
     if (KEYED) {
       const uint64_t rec = super0 + lane;
@@ -265,6 +362,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
       for (int b = 1; b < C::LOG2G; ++b) pw[b] = mul26(pw[b - 1], pw[b - 1]);
     }
   }
+  (void)own_cb;
 
 #pragma unroll 1
   for (int t = 0; t < C::G; ++t) {
@@ -307,15 +405,16 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     // Software pipeline: the ChaCha block of chunk kk+1 is independent of
     // the (serial) Poly1305 chain of chunk kk, so both sit in one basic
     // block and the scheduler interleaves them.
-    const uint32_t c0 = j * C::CPL;
+    const uint32_t c0 = j * C::CPL;  // first 64-B chunk of my span (in the record / segment)
+    const uint32_t cb = 1u + c0 + (SEG ? (uint32_t)__shfl((int)own_cb, src) : 0u);  // its counter
     const ChaPre pre = chacha_pre(kt, n_lo, n_hi);
     uint32_t ks[16];
-    chacha20_block_pre(kt, 1u + c0, pre, n_lo, n_hi, ks);
+    chacha20_block_pre(kt, cb, pre, n_lo, n_hi, ks);
 #pragma unroll
     for (int kk = 0; kk < C::CPL; ++kk) {
       const uint32_t c = c0 + kk;
       uint32_t ksn[16];
-      if (kk + 1 < C::CPL) chacha20_block_pre(kt, 2u + c, pre, n_lo, n_hi, ksn);
+      if (kk + 1 < C::CPL) chacha20_block_pre(kt, cb + 1u + kk, pre, n_lo, n_hi, ksn);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint32_t slot = swz(rho * C::SPR + 4u * c + q);
@@ -362,10 +461,21 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
       carry26(h);
       from26(h, p.h0, p.h1, p.h2, p.h3, p.h4);
     }
-    poly_block(p, 0u, 0u, (uint32_t)L, 0u);  // LE64(ad_len = 0) || LE64(L)
-    uint32_t tag[4];
-    poly_final(p, tag);
+    uint32_t tag[4] = {0u, 0u, 0u, 0u};
     const bool valid = rho < nv;
+    if (SEG) {
+      // the segment's partial sum (no length block, no s); lane 0 of the
+      // segment stores it
+      if (j == 0 && valid) {
+        const u32x4 w0 = {p.h0, p.h1, p.h2, p.h3}, w1 = {p.h4, 0u, 0u, 0u};
+        g_u32x4 *dp = (g_u32x4 *)(a.partial + (super0 + (uint64_t)t * C::RPT + rho));
+        __builtin_nontemporal_store(w0, dp);
+        __builtin_nontemporal_store(w1, dp + 1);
+      }
+    } else {
+      poly_block(p, 0u, 0u, (uint32_t)L, 0u);  // LE64(ad_len = 0) || LE64(L)
+      poly_final(p, tag);
+    }
     uint64_t fail_mask = 0;  // bit (r * G): record r of this tile is not output
     const uint64_t badk_mask = KEYED ? __ballot(j == 0 && bad_key) : 0ull;
     fail_mask = badk_mask;
@@ -373,7 +483,8 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     // that is inactive does not return that lane's value
     const uint32_t rec_di = MODE == kTileDesc ? (uint32_t)__shfl((int)own_di, src) : 0u;
     const bool rec_inplace = MODE == kTileDesc ? __shfl((int)own_inplace, src) != 0 : false;
-    if (DECRYPT) {
+    if (SEG) {
+    } else if (DECRYPT) {
       const uint4 want = lds[C::REC_SLOTS + rho];
       const uint32_t diff = (want.x ^ tag[0]) | (want.y ^ tag[1]) |
                             (want.z ^ tag[2]) | (want.w ^ tag[3]);
@@ -433,7 +544,12 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
       bool store = st[q];
       if (ABL == 1) store = store && (ov[q].x == 0x12345678u && ov[q].y == 0x9abcdef0u);
       uint8_t *dst;
-      if (MODE == kTileDesc) {
+      if (SEG) {  // output instruction q = segment q (OPR = 64): uniform offset
+        const uint32_t kl = (uint32_t)t * C::RPT + (uint32_t)q;
+        const uint64_t off = join64((uint32_t)__builtin_amdgcn_readlane((int)own_out_hi, (int)kl),
+                                    (uint32_t)__builtin_amdgcn_readlane((int)own_out_lo, (int)kl));
+        dst = out + off + 16u * pc;
+      } else if (MODE == kTileDesc) {
         const uint32_t rs = (uint32_t)t * C::RPT + (r < (uint32_t)C::RPT ? r : 0u);
         const uint64_t off = ((uint64_t)(uint32_t)__shfl((int)own_out_hi, rs) << 32) |
                              (uint32_t)__shfl((int)own_out_lo, rs);

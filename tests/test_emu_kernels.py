@@ -1,10 +1,13 @@
 """CPU-side check of the kernels' indexing: the unmodified records-path
-kernels (classification, tile / wave / lane-per-record) compiled as host C++
+kernels (classification, tile / long-record segments / lane-per-record) compiled as host C++
 against the HIP stand-in in tools/emu, run under AddressSanitizer on
-BASELINE config-4 shaped batches and compared with the oracle.  The grid is
-capped at 3 workgroups so every workgroup loops over several super-tiles /
+BASELINE config-4 shaped batches and compared with the oracle.  The emulation
+build classifies batches from 64 records (the product: 2048) and caps the
+grid at 3 workgroups so every workgroup loops over several super-tiles /
 batches; the gap puts records past 2^31 bytes into their buffers (64-bit
-offsets whose low word has bit 31 set).  Test infrastructure only: the
+offsets whose low word has bit 31 set); "ragged" lengths 1..70000 give odd
+segment tails and > 65535-byte records (generic class); a 300-segment
+scratch cap forces the segment-overflow path.  Test infrastructure only: the
 product runs these kernels on the GPU (tests/test_gpu_records_mixed.py)."""
 import os
 import subprocess
@@ -16,22 +19,44 @@ EMU = os.path.join(ROOT, "tools", "emu")
 BIN = os.path.join(EMU, "build", "emu_records")
 
 
-@pytest.fixture(scope="module")
-def emu_bin():
-    r = subprocess.run(["make", "-C", EMU, "GRID_CAP=3u"], capture_output=True, text=True,
-                       timeout=900)
+def _build(*extra):
+    r = subprocess.run(["make", "-C", EMU, "GRID_CAP=3u", *extra], capture_output=True,
+                       text=True, timeout=900)
     if r.returncode != 0:
         pytest.fail("emulation build failed:\n" + r.stdout[-2000:] + r.stderr[-4000:])
+
+
+@pytest.fixture(scope="module")
+def emu_bin():
+    _build()
     return BIN
 
 
+@pytest.fixture(scope="module")
+def emu_bin_small_cap():
+    _build("SEG_CAP=300ull")
+    return BIN + "_seg300ull"
+
+
+def _run(binary, mode, nrec, seed, gap):
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:allocator_may_return_null=1")
+    return subprocess.run([binary, mode, str(nrec), str(seed), str(gap)], capture_output=True,
+                          text=True, timeout=900, env=env)
+
+
 @pytest.mark.parametrize("mode,nrec,seed,gap", [
-    ("cfg4", 2300, 4, 0),
-    ("inplace", 2100, 5, (2 << 30) + 4096),
+    ("cfg4", 700, 4, 0),
+    ("inplace", 500, 5, (2 << 30) + 4096),
+    ("ragged", 300, 6, 0),
 ])
 def test_records_path_emulated(emu_bin, mode, nrec, seed, gap):
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:allocator_may_return_null=1")
-    r = subprocess.run([emu_bin, mode, str(nrec), str(seed), str(gap)], capture_output=True,
-                       text=True, timeout=900, env=env)
+    r = _run(emu_bin, mode, nrec, seed, gap)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]
+    assert "ok (0 failures)" in r.stdout
+
+
+def test_records_segment_overflow_emulated(emu_bin_small_cap):
+    # long records past the 300-segment scratch fall back to the generic kernel
+    r = _run(emu_bin_small_cap, "cfg4", 700, 7, 0)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]
     assert "ok (0 failures)" in r.stdout

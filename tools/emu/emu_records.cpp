@@ -9,6 +9,7 @@
 //                   top bucket 65519), packed 16-byte aligned, one key,
 //                   out-of-place encrypt + decrypt + tamper
 //     mode inplace: same lengths, encrypt and decrypt in place
+//     mode ragged : lengths uniform in 1..70000 (odd tails, > 65535 generic)
 //   emu_records <mode> <nrec> <seed> <gap>: records start <gap> bytes into
 //     each buffer (e.g. 4 GiB, to exercise 64-bit offsets)
 // Test infrastructure only (links oracle/chachapoly_oracle.c).
@@ -49,6 +50,7 @@ int main(int argc, char **argv) {
   const uint64_t R = argc > 2 ? std::strtoull(argv[2], nullptr, 0) : 3000;
   const uint64_t seed = argc > 3 ? std::strtoull(argv[3], nullptr, 0) : 4;
   const bool in_place = std::strcmp(mode, "inplace") == 0;
+  const bool ragged = std::strcmp(mode, "ragged") == 0;
   const uint64_t gap = argc > 4 ? std::strtoull(argv[4], nullptr, 0) : 0;
 
   double w[11], tot = 0;
@@ -63,6 +65,7 @@ int main(int argc, char **argv) {
       if (u < c) break;
     }
     lens[i] = k == 10 ? 65519u : (64u << k);
+    if (ragged) lens[i] = 1u + (uint32_t)(mix64(seed * 7 + i) % 70000u);  // long tails, > 65535
   }
   std::vector<noise_gpu_record> enc(R), dec(R);
   uint64_t in_off = gap, ct_off = gap;
@@ -96,7 +99,7 @@ int main(int argc, char **argv) {
 
   hipError_t e = noise_amd::launch_aead_records(false, d_key, 1, d_enc, R, pt, ct, nullptr, nullptr, nullptr);
   CHECK(e == hipSuccess, "encrypt launch %d", e);
-  std::vector<uint8_t> want(65536 + 16);
+  std::vector<uint8_t> want(70000 + 16);
   for (uint64_t i = 0; i < R; ++i) {
     const uint32_t L = lens[i];
     oracle_noise_encrypt(key, enc[i].nonce, nullptr, 0, pt_copy.data() + (enc[i].in_off - gap), L, want.data());

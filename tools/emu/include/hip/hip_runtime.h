@@ -144,6 +144,7 @@ inline uint64_t __ballot(int p) { return emu::ballot(p != 0); }
 
 // returns int, like the real builtin (so sign-extension bugs show here too)
 #define __builtin_amdgcn_readfirstlane(v) ((int)emu::shfl((uint32_t)(v), 0))
+#define __builtin_amdgcn_readlane(v, l) ((int)emu::shfl((uint32_t)(v), (int)(l)))
 #define __builtin_amdgcn_mbcnt_lo(m, c)                                          \
   ((uint32_t)(c) + (uint32_t)__builtin_popcount((uint32_t)(m) &                   \
        (emu::ctx.lane >= 32 ? 0xffffffffu : ((1u << emu::ctx.lane) - 1u))))
@@ -164,6 +165,13 @@ inline uint64_t __ballot(int p) { return emu::ballot(p != 0); }
 inline uint32_t __umul24(uint32_t a, uint32_t b) { return (a & 0xffffffu) * (b & 0xffffffu); }
 inline unsigned long long atomicAdd(unsigned long long *p, unsigned long long v) {
   return __atomic_fetch_add(p, v, __ATOMIC_SEQ_CST);
+}
+inline unsigned long long atomicMin(unsigned long long *p, unsigned long long v) {
+  unsigned long long old = __atomic_load_n(p, __ATOMIC_SEQ_CST);
+  while (v < old && !__atomic_compare_exchange_n(p, &old, v, false, __ATOMIC_SEQ_CST,
+                                                 __ATOMIC_SEQ_CST)) {
+  }
+  return old;
 }
 
 #define hipLaunchKernelGGL(kernel, grid, block, shmem, stream, ...)              \

@@ -42,7 +42,8 @@ constexpr int kClsLong = kNumTileCls;     // segmented long records
 constexpr int kClsGeneric = kNumTileCls + 1;
 constexpr int kNumCls = kNumTileCls + 2;
 constexpr int kColSegs = kNumCls;         // classifier column: full segments
-constexpr int kCols = 8;
+constexpr int kColTails = kNumCls + 1;    // classifier column: long records with a tail
+constexpr int kCols = kNumCls + 2;
 #ifndef NOISE_CLASSIFY_MIN  // overridable for the CPU emulation build
 #define NOISE_CLASSIFY_MIN 2048
 #endif
@@ -52,11 +53,13 @@ constexpr uint32_t kLongMax = 65535;      // the Noise message bound
 #define NOISE_SEG_CAP (1ull << 24)
 #endif
 constexpr uint64_t kSegCapMax = NOISE_SEG_CAP;  // 16 Mi segments = 16 GiB per call
-// Grid caps of the per-class launches (capped grids stride over their
-// work).  2048 single-wave workgroups = 8 per CU, what the register and LDS
-// budgets keep resident.  Overridable for the CPU emulation build (tools/emu).
+// Grid cap of the per-class launches, whose sizes are known only on the
+// device (capped grids stride over their work).  8192 single-wave workgroups
+// = 4x what the LDS budget keeps resident (8 per CU): the dispatcher refills
+// CUs as workgroups finish, which balanced config 4 best (2048: -6 %, 16384
+// and uncapped: -3 %, MI355X).  Overridable for the CPU emulation build.
 #ifndef NOISE_GRID_CAP
-#define NOISE_GRID_CAP 2048u
+#define NOISE_GRID_CAP 8192u
 #endif
 
 __device__ __forceinline__ int record_class(const noise_gpu_record &d,
@@ -79,11 +82,12 @@ __device__ __forceinline__ int record_class(const noise_gpu_record &d,
 
 // device header of the scratch buffer
 struct RecHdr {
-  unsigned long long counts[kCols];    // records per class; [kColSegs] = segments
+  unsigned long long counts[kCols];    // records per class; [kColSegs] = segments,
+                                       // [kColTails] = tails
   unsigned long long cls_base[kCols];  // start of each class in idx
   unsigned long long nlong;            // long records handled as segments
   unsigned long long nseg;             // their full segments
-  unsigned long long pad[14];
+  unsigned long long pad[30 - 2 * kCols];
 };
 static_assert(sizeof(RecHdr) == 256, "scratch header layout");
 
@@ -114,57 +118,51 @@ __global__ __launch_bounds__(64) void k_cls_count(
   const uint32_t lane = threadIdx.x;
   const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
   const uint64_t e0 = b0 + chunk < nrec ? b0 + chunk : nrec;
-  uint32_t cnt[kNumCls] = {0}, nseg = 0;
+  uint32_t cnt[kNumCls] = {0}, nseg = 0, ntail = 0;
 #pragma unroll 1
   for (uint64_t i0 = b0; i0 < e0; i0 += 64) {
     const uint64_t i = i0 + lane;
     int cls = -1;
     uint32_t nf = 0;
+    bool tail = false;
     if (i < e0) {
       const noise_gpu_record d = recs[i];
       cls = record_class(d, nkeys, in, out);
       nf = cls == kClsLong ? d.len >> 10 : 0u;
+      tail = cls == kClsLong && (d.len & 1023u) != 0;
     }
 #pragma unroll
     for (int c = 0; c < kNumCls; ++c) cnt[c] += (uint32_t)__builtin_popcountll(__ballot(cls == c));
     nseg += wave_sum(nf);
+    ntail += (uint32_t)__builtin_popcountll(__ballot(tail));
   }
   if (lane < (uint32_t)kCols) {
-    uint32_t v = nseg;
+    uint32_t v = lane == (uint32_t)kColSegs ? nseg : ntail;
 #pragma unroll
     for (int c = 0; c < kNumCls; ++c) v = lane == (uint32_t)c ? cnt[c] : v;
     part[(uint64_t)blockIdx.x * kCols + lane] = v;
   }
 }
 
+// one workgroup per column
 __global__ __launch_bounds__(64) void k_cls_scan(const uint32_t *part, uint32_t nw,
                                                  unsigned long long *wbase,
                                                  RecHdr *hdr, uint64_t segcap) {
-  const uint32_t lane = threadIdx.x;
-  unsigned long long tot[kCols];
+  const uint32_t lane = threadIdx.x, c = blockIdx.x;
+  unsigned long long run = 0;
 #pragma unroll 1
-  for (int c = 0; c < kCols; ++c) {
-    unsigned long long run = 0;
-#pragma unroll 1
-    for (uint32_t w0 = 0; w0 < nw; w0 += 64) {
-      const uint32_t w = w0 + lane;
-      const uint32_t v = w < nw ? part[(uint64_t)w * kCols + c] : 0u;
-      const uint32_t inc = wave_incl_scan(v, lane);
-      if (w < nw) wbase[(uint64_t)w * kCols + c] = run + inc - v;
-      run += (uint32_t)__shfl((int)inc, 63);
-    }
-    tot[c] = run;
+  for (uint32_t w0 = 0; w0 < nw; w0 += 64) {
+    const uint32_t w = w0 + lane;
+    const uint32_t v = w < nw ? part[(uint64_t)w * kCols + c] : 0u;
+    const uint32_t inc = wave_incl_scan(v, lane);
+    if (w < nw) wbase[(uint64_t)w * kCols + c] = run + inc - v;
+    run += (uint32_t)__shfl((int)inc, 63);
   }
   if (lane == 0) {
-    unsigned long long b = 0;
-    for (int c = 0; c < kCols; ++c) {
-      hdr->counts[c] = tot[c];
-      hdr->cls_base[c] = c < kNumCls ? b : 0ull;
-      if (c < kNumCls) b += tot[c];
-    }
+    hdr->counts[c] = run;
     // lowered by k_cls_scatter if the segment scratch overflows
-    hdr->nlong = tot[kClsLong];
-    hdr->nseg = tot[kColSegs] < segcap ? tot[kColSegs] : segcap;
+    if (c == (uint32_t)kClsLong) hdr->nlong = run;
+    if (c == (uint32_t)kColSegs) hdr->nseg = run < segcap ? run : segcap;
   }
 }
 
@@ -172,7 +170,7 @@ __global__ __launch_bounds__(64) void k_cls_scatter(
     const noise_gpu_record *__restrict__ recs, uint64_t nrec, uint32_t chunk,
     uint32_t nkeys, const uint8_t *in, const uint8_t *out,
     const unsigned long long *wbase, RecHdr *hdr, uint32_t *idx, SegRec *rt,
-    SegEntry *segs, uint64_t segcap) {
+    SegEntry *segs, uint32_t *tails, uint64_t segcap) {
   const uint32_t lane = threadIdx.x;
   const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
   const uint64_t e0 = b0 + chunk < nrec ? b0 + chunk : nrec;
@@ -180,8 +178,20 @@ __global__ __launch_bounds__(64) void k_cls_scatter(
 #pragma unroll
   for (int c = 0; c < kCols; ++c) run[c] = wbase[(uint64_t)blockIdx.x * kCols + c];
   unsigned long long cbase[kNumCls];
+  {
+    unsigned long long b = 0;
 #pragma unroll
-  for (int c = 0; c < kNumCls; ++c) cbase[c] = hdr->cls_base[c];
+    for (int c = 0; c < kNumCls; ++c) {
+      cbase[c] = b;
+      b += hdr->counts[c];
+    }
+  }
+  if (blockIdx.x == 0 && lane < (uint32_t)kNumCls) {
+    unsigned long long b = cbase[0];
+#pragma unroll
+    for (int c = 0; c < kNumCls; ++c) b = lane == (uint32_t)c ? cbase[c] : b;
+    hdr->cls_base[lane] = b;
+  }
   bool overflow = false;
   unsigned long long ov_q = ~0ull, ov_seg = ~0ull;
 #pragma unroll 1
@@ -194,6 +204,7 @@ __global__ __launch_bounds__(64) void k_cls_scatter(
       cls = record_class(d, nkeys, in, out);
     }
     const uint32_t nf = cls == kClsLong ? d.len >> 10 : 0u;
+    const bool tail = cls == kClsLong && (d.len & 1023u) != 0;
     unsigned long long q = 0;
 #pragma unroll
     for (int c = 0; c < kNumCls; ++c) {
@@ -205,6 +216,14 @@ __global__ __launch_bounds__(64) void k_cls_scatter(
         idx[cbase[c] + q] = (uint32_t)i;
       }
       run[c] += (unsigned long long)__builtin_popcountll(m);
+    }
+    {  // long records with a tail: the tail list (record order)
+      const uint64_t m = __ballot(tail);
+      if (tail)
+        tails[run[kColTails] + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+            (uint32_t)q;
+      run[kColTails] += (unsigned long long)__builtin_popcountll(m);
     }
     // long records: header fields of their SegRec, first segment index
     const uint32_t inc = wave_incl_scan(nf, lane);
@@ -273,31 +292,102 @@ __global__ __launch_bounds__(64) void k_seg_prep(const uint8_t *__restrict__ key
                    r2 = otk[2] & 0x0ffffffcu, r3 = otk[3] & 0x0ffffffcu;
     R.r[0] = r0; R.r[1] = r1; R.r[2] = r2; R.r[3] = r3;
     R.s[0] = otk[4]; R.s[1] = otk[5]; R.s[2] = otk[6]; R.s[3] = otk[7];
-    F26 x = to26(r0, r1, r2, r3, 0u);
-    x = mul26(x, x);  // r^2
-    x = mul26(x, x);  // r^4
-    x = mul26(x, x);  // r^8
-    x = mul26(x, x);  // r^16
+    // squaring chain r^(2^b); r^(tail blocks) = product over the bits of
+    // the tail's Poly1305 block count (1..64)
+    const uint32_t nbt = ((R.len & 1023u) + 15u) >> 4;
+    F26 x = to26(r0, r1, r2, r3, 0u), rt_pow;
+    rt_pow.a[0] = 1u;
+    rt_pow.a[1] = rt_pow.a[2] = rt_pow.a[3] = rt_pow.a[4] = 0u;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      if ((nbt >> b) & 1u) rt_pow = mul26(rt_pow, x);
+      x = mul26(x, x);
+    }
+    // x = r^16
+    if ((nbt >> 4) & 1u) rt_pow = mul26(rt_pow, x);
     const F26 x32 = mul26(x, x), x64 = mul26(x32, x32);
+    if ((nbt >> 5) & 1u) rt_pow = mul26(rt_pow, x32);
+    if ((nbt >> 6) & 1u) rt_pow = mul26(rt_pow, x64);  // a 1009..1023-byte tail: 64 blocks
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
       R.pw16[i] = x.a[i];
       R.pw32[i] = x32.a[i];
       R.r64[i] = x64.a[i];
+      R.rtail[i] = rt_pow.a[i];
     }
   }
 }
 
+// k_seg_tail: lane per tail (a long record's len % 1024 bytes past its last
+// full segment; ChaCha counters from 1 + 16 nfull).  Encrypts / decrypts the
+// tail and leaves its Poly1305 sum P_tail (Horner from 0 over the tail's
+// ciphertext blocks, the last one zero padded) in the SegRec.  Decrypt
+// writes the plaintext unconditionally, like the segment kernel: k_seg_fixup
+// reverts a record whose tag fails.
+template <bool DECRYPT>
+__global__ __launch_bounds__(64) void k_seg_tail(const uint32_t *__restrict__ tails,
+                                                 SegRec *rt, const RecHdr *hdr,
+                                                 const uint8_t *in, uint8_t *out) {
+  const uint64_t n = hdr->counts[kColTails], nlong = hdr->nlong;
+#pragma unroll 1
+  for (uint64_t t = (uint64_t)blockIdx.x * 64 + threadIdx.x; t < n;
+       t += (uint64_t)gridDim.x * 64) {
+    const uint32_t q = tails[t];
+    if (q >= nlong) continue;  // beyond the segment scratch: generic kernel
+    SegRec &R = rt[q];
+    uint32_t k[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) k[i] = R.k[i];
+    Poly1305 p;
+    p.r0 = R.r[0]; p.r1 = R.r[1]; p.r2 = R.r[2]; p.r3 = R.r[3];
+    p.rr0 = (p.r0 >> 2) * 5u;
+    p.rr1 = p.r1 + (p.r1 >> 2);
+    p.rr2 = p.r2 + (p.r2 >> 2);
+    p.rr3 = p.r3 + (p.r3 >> 2);
+    p.r0lo = p.r0 & 3u;
+    p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0u;
+    const uint32_t nf = R.nfull, tb = R.len - 1024u * nf;
+    const uint8_t *src = in + R.in_off + 1024ull * nf;
+    uint8_t *dst = out + R.out_off + 1024ull * nf;
+    const uint32_t n_lo = (uint32_t)R.nonce, n_hi = (uint32_t)(R.nonce >> 32);
+#pragma unroll 1
+    for (uint32_t off = 0; off < tb; off += 64) {
+      uint32_t ks[16];
+      chacha20_block(k, 1u + 16u * nf + (off >> 6), n_lo, n_hi, ks);
+      uint4 v[4];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {  // the chunk's loads first (independent)
+        const int m = (int)(tb - off) - 16 * w;
+        const int nb = m >= 16 ? 16 : (m > 0 ? m : 0);
+        v[w] = nb == 16 ? load16<true>(src + off + 16 * w, 16)
+                        : load16<false>(src + off + 16 * w, nb);
+      }
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const int m = (int)(tb - off) - 16 * w;
+        if (m <= 0) break;
+        const int nb = m >= 16 ? 16 : m;
+        const uint4 o = mask_bytes(make_uint4(v[w].x ^ ks[4 * w], v[w].y ^ ks[4 * w + 1],
+                                              v[w].z ^ ks[4 * w + 2], v[w].w ^ ks[4 * w + 3]), nb);
+        if (DECRYPT) poly_block(p, v[w].x, v[w].y, v[w].z, v[w].w);
+        else poly_block(p, o.x, o.y, o.z, o.w);
+        if (nb == 16) store16<true>(dst + off + 16 * w, o, 16);
+        else store16<false>(dst + off + 16 * w, o, nb);
+      }
+    }
+    R.ptail[0] = p.h0; R.ptail[1] = p.h1; R.ptail[2] = p.h2; R.ptail[3] = p.h3;
+    R.ptail[4] = p.h4;
+  }
+}
+
 // k_seg_finalize: lane per long record.  h = Horner over the segments'
-// partial sums in R = r^64, then the tail (len % 1024 bytes, ChaCha counters
-// from 1 + 16 nfull) lane-serially, the length block and the tag.  Decrypt
-// verifies the tag first (MAC over the tail ciphertext), decrypts the tail
-// only if it matches, and writes the record's status.
+// partial sums in R = r^64, then h r^(tail blocks) + P_tail, the length
+// block and the tag.  Encrypt stores the tag; decrypt compares it and writes
+// the record's status.
 template <bool DECRYPT>
 __global__ __launch_bounds__(64) void k_seg_finalize(
-    const uint8_t *__restrict__ keys, const SegRec *__restrict__ rt,
-    const SegPartial *__restrict__ partial, const RecHdr *hdr,
-    const uint8_t *in, uint8_t *out, uint8_t *status) {
+    const SegRec *__restrict__ rt, const SegPartial *__restrict__ partial,
+    const RecHdr *hdr, const uint8_t *in, uint8_t *out, uint8_t *status) {
   const uint64_t n = hdr->nlong;
 #pragma unroll 1
   for (uint64_t q = (uint64_t)blockIdx.x * 64 + threadIdx.x; q < n;
@@ -320,6 +410,17 @@ __global__ __launch_bounds__(64) void k_seg_finalize(
       for (int i = 0; i < 5; ++i) acc.a[i] += t.a[i];
       carry26(acc);
     }
+    const uint32_t len = R.len;
+    if (len & 1023u) {
+      F26 rtp;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) rtp.a[i] = R.rtail[i];
+      acc = mul26(acc, rtp);
+      const F26 t = to26(R.ptail[0], R.ptail[1], R.ptail[2], R.ptail[3], R.ptail[4]);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) acc.a[i] += t.a[i];
+    }
+    carry26(acc);
     carry26(acc);
     Poly1305 p;
     from26(acc, p.h0, p.h1, p.h2, p.h3, p.h4);
@@ -330,119 +431,74 @@ __global__ __launch_bounds__(64) void k_seg_finalize(
     p.rr3 = p.r3 + (p.r3 >> 2);
     p.r0lo = p.r0 & 3u;
     p.s0 = R.s[0]; p.s1 = R.s[1]; p.s2 = R.s[2]; p.s3 = R.s[3];
-
-    uint32_t k[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) k[i] = R.k[i];
-    const uint32_t n_lo = (uint32_t)R.nonce, n_hi = (uint32_t)(R.nonce >> 32);
-    const uint32_t len = R.len, tb = len - 1024u * nf;
-    const uint8_t *src = in + R.in_off + 1024ull * nf;
-    uint8_t *dst = out + R.out_off + 1024ull * nf;
-    const uint32_t cb = 1u + 16u * nf;
-
+    poly_block(p, 0u, 0u, len, 0u);  // LE64(ad_len = 0) || LE64(len)
+    uint32_t tag[4];
+    poly_final(p, tag);
     if (!DECRYPT) {
-#pragma unroll 1
-      for (uint32_t off = 0; off < tb; off += 64) {
-        uint32_t ks[16];
-        chacha20_block(k, cb + (off >> 6), n_lo, n_hi, ks);
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          const int m = (int)(tb - off) - 16 * w;
-          if (m <= 0) break;
-          const int nb = m >= 16 ? 16 : m;
-          const uint4 v = nb == 16 ? load16<true>(src + off + 16 * w, 16)
-                                   : load16<false>(src + off + 16 * w, nb);
-          const uint4 o = mask_bytes(make_uint4(v.x ^ ks[4 * w], v.y ^ ks[4 * w + 1],
-                                                v.z ^ ks[4 * w + 2], v.w ^ ks[4 * w + 3]), nb);
-          poly_block(p, o.x, o.y, o.z, o.w);
-          if (nb == 16) store16<true>(dst + off + 16 * w, o, 16);
-          else store16<false>(dst + off + 16 * w, o, nb);
-        }
-      }
-      poly_block(p, 0u, 0u, len, 0u);  // LE64(ad_len = 0) || LE64(len)
-      uint32_t tag[4];
-      poly_final(p, tag);
       uint8_t *tp = out + R.out_off + len;
       if ((len & 15u) == 0) store16<true>(tp, make_uint4(tag[0], tag[1], tag[2], tag[3]), 16);
       else store16<false>(tp, make_uint4(tag[0], tag[1], tag[2], tag[3]), 16);
     } else {
-      // MAC over the tail ciphertext, then the length block and the tag
-#pragma unroll 1
-      for (uint32_t off = 0; off < tb; off += 16) {
-        const uint32_t nb = tb - off >= 16 ? 16u : tb - off;
-        const uint4 v = nb == 16 ? load16<true>(src + off, 16) : load16<false>(src + off, (int)nb);
-        poly_block(p, v.x, v.y, v.z, v.w);
-      }
-      poly_block(p, 0u, 0u, len, 0u);
-      uint32_t tag[4];
-      poly_final(p, tag);
       const uint8_t *tp = in + R.in_off + len;
       const uint4 want = (len & 15u) == 0 ? load16<true>(tp, 16) : load16<false>(tp, 16);
       const uint32_t diff = (want.x ^ tag[0]) | (want.y ^ tag[1]) | (want.z ^ tag[2]) |
                             (want.w ^ tag[3]);
-      const bool ok = diff == 0u;
-      const bool in_place = src == dst;
-      if (ok || !in_place) {
-#pragma unroll 1
-        for (uint32_t off = 0; off < tb; off += 64) {
-          uint32_t ks[16];
-          if (ok) chacha20_block(k, cb + (off >> 6), n_lo, n_hi, ks);
-#pragma unroll
-          for (int w = 0; w < 4; ++w) {
-            const int m = (int)(tb - off) - 16 * w;
-            if (m <= 0) break;
-            const int nb = m >= 16 ? 16 : m;
-            uint4 o = make_uint4(0u, 0u, 0u, 0u);  // failed copy: zeroed
-            if (ok) {
-              const uint4 v = nb == 16 ? load16<true>(src + off + 16 * w, 16)
-                                       : load16<false>(src + off + 16 * w, nb);
-              o = make_uint4(v.x ^ ks[4 * w], v.y ^ ks[4 * w + 1], v.z ^ ks[4 * w + 2],
-                             v.w ^ ks[4 * w + 3]);
-            }
-            if (nb == 16) store16<true>(dst + off + 16 * w, o, 16);
-            else store16<false>(dst + off + 16 * w, o, nb);
-          }
-        }
-      }
-      status[R.di] = ok ? NOISE_GPU_REC_OK : NOISE_GPU_REC_BAD_MAC;
+      status[R.di] = diff == 0u ? NOISE_GPU_REC_OK : NOISE_GPU_REC_BAD_MAC;
     }
   }
 }
 
-// k_seg_fixup (decrypt): lane per full segment.  The segment kernel wrote
-// plaintext before the tag was known; for a record whose tag failed, put
-// the ciphertext back (in place: XOR the keystream again, leaving the buffer
-// as it was -- crypto_aead_read semantics) or zero the copy.
+// k_seg_fixup (decrypt): lane per full segment, then lane per tail.  The
+// segment and tail kernels wrote plaintext before the tag was known; for a
+// record whose tag failed, put the ciphertext back (in place: XOR the
+// keystream again, leaving the buffer as it was -- crypto_aead_read
+// semantics) or zero the copy.
 __global__ __launch_bounds__(64) void k_seg_fixup(
-    const uint8_t *__restrict__ keys, const SegEntry *__restrict__ segs,
+    const SegEntry *__restrict__ segs, const uint32_t *__restrict__ tails,
     const SegRec *__restrict__ rt, const RecHdr *hdr, const uint8_t *in,
     uint8_t *out, const uint8_t *status) {
-  const uint64_t n = hdr->nseg;
+  const uint64_t nseg = hdr->nseg, ntail = hdr->counts[kColTails], nlong = hdr->nlong;
 #pragma unroll 1
-  for (uint64_t g = (uint64_t)blockIdx.x * 64 + threadIdx.x; g < n;
+  for (uint64_t g = (uint64_t)blockIdx.x * 64 + threadIdx.x; g < nseg + ntail;
        g += (uint64_t)gridDim.x * 64) {
-    const SegEntry e = segs[g];
-    const SegRec &R = rt[e.q];
+    uint32_t q, c0, nbytes;
+    if (g < nseg) {
+      const SegEntry e = segs[g];
+      q = e.q;
+      c0 = 16u * e.s;
+      nbytes = 1024u;
+    } else {
+      q = tails[g - nseg];
+      if (q >= nlong) continue;
+      c0 = 16u * rt[q].nfull;
+      nbytes = rt[q].len & 1023u;
+    }
+    const SegRec &R = rt[q];
     if (status[R.di] == NOISE_GPU_REC_OK) continue;
-    uint8_t *dst = out + R.out_off + 1024ull * e.s;
+    uint8_t *dst = out + R.out_off + 64ull * c0;
     const bool in_place = in + R.in_off == out + R.out_off;
     uint32_t k[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) k[i] = R.k[i];
 #pragma unroll 1
-    for (uint32_t c = 0; c < 16; ++c) {
+    for (uint32_t off = 0; off < nbytes; off += 64) {
       uint32_t ks[16];
       if (in_place)
-        chacha20_block(k, 1u + 16u * e.s + c, (uint32_t)R.nonce, (uint32_t)(R.nonce >> 32), ks);
+        chacha20_block(k, 1u + c0 + (off >> 6), (uint32_t)R.nonce, (uint32_t)(R.nonce >> 32), ks);
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
+        const int m = (int)(nbytes - off) - 16 * w;
+        if (m <= 0) break;
+        const int nb = m >= 16 ? 16 : m;
         uint4 o = make_uint4(0u, 0u, 0u, 0u);
         if (in_place) {
-          const uint4 v = load16<true>(dst + 64u * c + 16 * w, 16);
+          const uint4 v = nb == 16 ? load16<true>(dst + off + 16 * w, 16)
+                                   : load16<false>(dst + off + 16 * w, nb);
           o = make_uint4(v.x ^ ks[4 * w], v.y ^ ks[4 * w + 1], v.z ^ ks[4 * w + 2],
                          v.w ^ ks[4 * w + 3]);
         }
-        store16<true>(dst + 64u * c + 16 * w, o, 16);
+        if (nb == 16) store16<true>(dst + off + 16 * w, o, 16);
+        else store16<false>(dst + off + 16 * w, o, nb);
       }
     }
   }
@@ -533,8 +589,9 @@ static inline unsigned capped(uint64_t want, uint64_t cap) {
 
 template <bool DECRYPT>
 static void launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr *hdr,
-                           const uint8_t *keys, uint64_t segbound, const uint8_t *in,
-                           uint8_t *out, uint8_t *status, hipStream_t stream) {
+                           const uint8_t *keys, const uint32_t *tails, uint64_t segbound,
+                           const uint8_t *in, uint8_t *out, uint8_t *status,
+                           hipStream_t stream) {
   const dim3 bt(64);
   const dim3 grid(capped((nrec + 63) / 64, NOISE_GRID_CAP));
   TileArgs a = ta;
@@ -547,15 +604,20 @@ static void launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr *hdr,
   NOISE_DESC_TILE(3, 256)
   NOISE_DESC_TILE(4, 512)
 #undef NOISE_DESC_TILE
-  // long records: prep -> every full segment in one tile launch -> finalize
-  hipLaunchKernelGGL(k_seg_prep, grid, bt, 0, stream, keys, const_cast<SegRec *>(ta.rt), hdr);
+  // long records: prep -> every full segment in one tile launch + the tails
+  // -> finalize (-> decrypt: fix-up of records whose tag failed)
+  SegRec *rt = const_cast<SegRec *>(ta.rt);
+  hipLaunchKernelGGL(k_seg_prep, grid, bt, 0, stream, keys, rt, hdr);
   const dim3 gseg(capped((segbound + 63) / 64, NOISE_GRID_CAP));
   hipLaunchKernelGGL((k_aead_tile<DECRYPT, 1024, false, kTileSeg>), gseg, bt, 0, stream, a);
-  hipLaunchKernelGGL((k_seg_finalize<DECRYPT>), grid, bt, 0, stream, keys, ta.rt, ta.partial,
-                     hdr, in, out, status);
-  if (DECRYPT)
-    hipLaunchKernelGGL(k_seg_fixup, gseg, bt, 0, stream, keys, ta.segs, ta.rt, hdr, in, out,
+  hipLaunchKernelGGL((k_seg_tail<DECRYPT>), grid, bt, 0, stream, tails, rt, hdr, in, out);
+  hipLaunchKernelGGL((k_seg_finalize<DECRYPT>), grid, bt, 0, stream, ta.rt, ta.partial, hdr,
+                     in, out, status);
+  if (DECRYPT) {
+    const dim3 gfix(capped((segbound + nrec + 63) / 64, NOISE_GRID_CAP));
+    hipLaunchKernelGGL(k_seg_fixup, gfix, bt, 0, stream, ta.segs, tails, ta.rt, hdr, in, out,
                        status);
+  }
 }
 
 hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
@@ -581,12 +643,13 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   const uint64_t nw = (nrec + chunk - 1) / chunk;
   const uint64_t segcap = nrec * 63 < kSegCapMax ? nrec * 63 : kSegCapMax;
 
-  // scratch: header | part[nw][8] | wbase[nw][8] | idx[nrec] | rt[nrec] |
-  //          segs[segcap] | partial[segcap]
+  // scratch: header | part[nw][kCols] | wbase[nw][kCols] | idx[nrec] |
+  //          tails[nrec] | rt[nrec] | segs[segcap] | partial[segcap]
   const uint64_t o_part = sizeof(RecHdr);
   const uint64_t o_wbase = align_up(o_part + nw * kCols * 4, 256);
   const uint64_t o_idx = align_up(o_wbase + nw * kCols * 8, 256);
-  const uint64_t o_rt = align_up(o_idx + nrec * 4, 256);
+  const uint64_t o_tails = align_up(o_idx + nrec * 4, 256);
+  const uint64_t o_rt = align_up(o_tails + nrec * 4, 256);
   const uint64_t o_segs = align_up(o_rt + nrec * sizeof(SegRec), 256);
   const uint64_t o_part2 = align_up(o_segs + segcap * sizeof(SegEntry), 256);
   const uint64_t bytes = o_part2 + segcap * sizeof(SegPartial);
@@ -598,14 +661,15 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   uint32_t *part = reinterpret_cast<uint32_t *>(base + o_part);
   unsigned long long *wbase = reinterpret_cast<unsigned long long *>(base + o_wbase);
   uint32_t *idx = reinterpret_cast<uint32_t *>(base + o_idx);
+  uint32_t *tails = reinterpret_cast<uint32_t *>(base + o_tails);
   SegRec *rt = reinterpret_cast<SegRec *>(base + o_rt);
   SegEntry *segs = reinterpret_cast<SegEntry *>(base + o_segs);
   SegPartial *partial = reinterpret_cast<SegPartial *>(base + o_part2);
 
   const dim3 b64(64);
   hipLaunchKernelGGL(k_cls_count, dim3((unsigned)nw), b64, 0, stream, recs, nrec, (uint32_t)chunk, nkeys, in, out, part);
-  hipLaunchKernelGGL(k_cls_scan, dim3(1), b64, 0, stream, part, (uint32_t)nw, wbase, hdr, segcap);
-  hipLaunchKernelGGL(k_cls_scatter, dim3((unsigned)nw), b64, 0, stream, recs, nrec, (uint32_t)chunk, nkeys, in, out, wbase, hdr, idx, rt, segs, segcap);
+  hipLaunchKernelGGL(k_cls_scan, dim3(kCols), b64, 0, stream, part, (uint32_t)nw, wbase, hdr, segcap);
+  hipLaunchKernelGGL(k_cls_scatter, dim3((unsigned)nw), b64, 0, stream, recs, nrec, (uint32_t)chunk, nkeys, in, out, wbase, hdr, idx, rt, segs, tails, segcap);
 
   TileArgs ta{};
   ta.in = in;
@@ -621,8 +685,8 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   ta.rt = rt;
   ta.partial = partial;
   ta.nseg = &hdr->nseg;
-  if (decrypt) launch_classes<true>(ta, nrec, hdr, keys, segcap, in, out, status, stream);
-  else launch_classes<false>(ta, nrec, hdr, keys, segcap, in, out, status, stream);
+  if (decrypt) launch_classes<true>(ta, nrec, hdr, keys, tails, segcap, in, out, status, stream);
+  else launch_classes<false>(ta, nrec, hdr, keys, tails, segcap, in, out, status, stream);
 
   const dim3 gg((unsigned)(gblocks < 2 * NOISE_GRID_CAP ? gblocks : 2 * NOISE_GRID_CAP));
   if (decrypt)

@@ -82,17 +82,21 @@ enum TileMode : int {
 // load-balanced launch -- and leaves the segment's Poly1305 Horner sum
 //   P_s = sum_{i<64} m_{64s+i} r^(64-i)
 // in SegPartial.  The finalize kernel combines h = sum_s P_s r^(64(nfull-1-s))
-// (Horner in R = r^64), runs the tail, the length block and the tag.
-struct SegRec {                  // one per long record, 176 B
+// (Horner in R = r^64), appends the tail (k_seg_tail: the len % 1024 bytes
+// past the last full segment, one lane per tail) as h r^(tail blocks) +
+// P_tail, then the length block and the tag.
+struct SegRec {                  // one per long record, 224 B
   uint64_t in_off, out_off, nonce, seg0;  // seg0: index of segment 0
   uint32_t k[8];                 // the record's key (copied from the key table)
   uint32_t key_idx, di, len, nfull;       // di: descriptor index
   uint32_t r[4];                 // clamped Poly1305 r (radix 2^32)
   uint32_t s[4];                 // Poly1305 s
   uint32_t pw16[5], pw32[5], r64[5];      // r^16, r^32, r^64 (radix 2^26)
-  uint32_t pad;
+  uint32_t rtail[5];             // r^(tail blocks) (radix 2^26)
+  uint32_t ptail[5];             // the tail's Poly1305 sum (radix 2^32, h4 small)
+  uint32_t pad[3];
 };
-static_assert(sizeof(SegRec) == 176, "SegRec layout");
+static_assert(sizeof(SegRec) == 224, "SegRec layout");
 struct SegEntry {                // one per full segment
   uint32_t q, s;                 // long-record index, segment number
 };

@@ -1,8 +1,9 @@
 """GPU parity for descriptor batches big enough to take the classified path
-(records_kernels.hip): tile classes, the one-wave-per-record class (> 16 KiB,
-any length incl. 65519) and the generic lane-per-record class (AD, odd
-lengths, unaligned offsets, bad key index), all in ONE batch, against the
-CPU oracle.  Bit-exact."""
+(records_kernels.hip): tile classes (64..512 B), long records cut into 1 KiB
+segments + tails (1024..65535 B, any length: tails of 1..1023 bytes, 64-block
+tails, the 65519 Noise maximum) and the generic lane-per-record class (AD,
+odd lengths, unaligned offsets, bad key index, > 65535 B), all in ONE batch,
+against the CPU oracle.  Bit-exact."""
 import random
 
 import numpy as np
@@ -14,7 +15,8 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 TILE = [64, 128, 192, 256, 512, 1024, 2048, 4096, 8192, 16384]
-WAVE = [16385, 16400, 20000, 32768, 40001, 65519, 65520, 49152 + 7]
+WAVE = [16385, 16400, 20000, 32768, 40001, 65519, 65520, 49152 + 7, 1025, 2047, 3071, 65535,
+        70000, 1024 * 9 + 1009]
 GENERIC = [0, 1, 15, 17, 100, 1000, 3000, 5000, 16383]
 
 

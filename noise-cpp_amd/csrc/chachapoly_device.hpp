@@ -300,6 +300,12 @@ __device__ __forceinline__ uint64_t join64(uint32_t hi, uint32_t lo) {
 __device__ __forceinline__ void wait_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
 __device__ __forceinline__ void wait_lds() { __builtin_amdgcn_s_waitcnt(0xC07F); }   // lgkmcnt(0)
 __device__ __forceinline__ void wait_all() { __builtin_amdgcn_s_waitcnt(0x0070); }   // both
+// vmcnt(N): all but the wave's N youngest vector-memory operations done
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);  // expcnt, lgkmcnt: no wait
+}
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // Record buffers are device (global) memory.  Naming the address space keeps
@@ -307,6 +313,37 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // pointer to a kernel argument (e.g. base + an offset read from a
 // descriptor); FLAT stores also count against lgkmcnt.
 typedef __attribute__((address_space(1))) u32x4 g_u32x4;
+
+// LDS-DMA of 16 bytes per lane: global -> LDS at lds_base + 16 * lane
+// (global_load_lds_dwordx4, M0 = the wave-uniform LDS byte address).  Issued
+// from inline asm so that the compiler does not see an LDS write in flight:
+// otherwise it drains vmcnt(0) before the first ds_read of ANY part of the
+// LDS array, which would serialise a DMA into the other tile buffer with the
+// compute on this one.  Every reader of a DMA'd buffer therefore waits with
+// an explicit s_waitcnt vmcnt (wait_vmem / wait_vmcnt) and a wave fence.
+// sbase: wave-uniform 64-bit base (SGPRs) + per-lane 32-bit offset; vaddr:
+// per-lane 64-bit address.  Host builds (tools/emu) use the builtin.
+typedef __attribute__((address_space(3))) void lds_void;
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void lds_dma16_s(const void *sbase, uint32_t voff,
+                                            lds_void *lds_base) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(NOISE_DMA_BUILTIN)
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+               :: "v"(voff), "s"(sbase), "s"((uint32_t)(uintptr_t)lds_base) : "memory", "m0");
+#else
+  __builtin_amdgcn_global_load_lds((const void *)((const uint8_t *)sbase + voff), lds_base, 16, 0, 0);
+#endif
+}
+__device__ __forceinline__ void lds_dma16_v(const void *vaddr, lds_void *lds_base) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(NOISE_DMA_BUILTIN)
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+               :: "v"(vaddr), "s"((uint32_t)(uintptr_t)lds_base) : "memory", "m0");
+#else
+  __builtin_amdgcn_global_load_lds(vaddr, lds_base, 16, 0, 0);
+#endif
+}
+#pragma clang diagnostic pop
 
 // Byte-granular little-endian word load/store for unaligned records.
 __device__ __forceinline__ uint32_t ld_bytes(const uint8_t *p, int n) {

@@ -158,25 +158,20 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
     // slot s = 64q + lane holds piece swz(s) = 64q + gl[q & 3]; packed
     // records put piece g of an encrypt tile at byte 16g and of a decrypt
     // tile (SPR+1 pieces per record) at 16(g + g/SPR).
-    const uint8_t *base = in + rec0 * in_stride;
+    const uint8_t *base = in + rec0 * in_stride;  // wave-uniform
 #pragma unroll
     for (int q = 0; q < C::REC_SLOTS / 64; ++q) {
       const uint32_t g = 64u * q + gl[q & 3];
       const uint32_t rr = g / C::SPR;
       const uint32_t off = DECRYPT ? 16u * (g + rr) : 16u * g;
-      if (rr < nv)
-        __builtin_amdgcn_global_load_lds(
-            (const void *)(base + off),
-            (__attribute__((address_space(3))) void *)(lds3 + 64 * q), 16, 0, 0);
+      if (rr < nv) lds_dma16_s(base, off, (lds_void *)(lds3 + 64 * q));
     }
     if (TAGGED_IN) {  // tag pieces: slot REC_SLOTS + r <- piece (r, SPR)
 #pragma unroll
       for (int q = C::REC_SLOTS / 64; q < (C::NSLOT + 63) / 64; ++q) {
         const uint32_t r = 64u * q + lane - C::REC_SLOTS;
         if (r < nv)
-          __builtin_amdgcn_global_load_lds(
-              (const void *)(base + 16u * (r * (C::SPR + 1) + C::SPR)),
-              (__attribute__((address_space(3))) void *)(lds3 + 64 * q), 16, 0, 0);
+          lds_dma16_s(base, 16u * (r * (C::SPR + 1) + C::SPR), (lds_void *)(lds3 + 64 * q));
       }
     }
   } else if (MODE == kTileSeg) {
@@ -189,9 +184,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
         const uint32_t kl = t_rpt + q;
         const uint64_t off = join64((uint32_t)__builtin_amdgcn_readlane((int)own_in_hi, (int)kl),
                                     (uint32_t)__builtin_amdgcn_readlane((int)own_in_lo, (int)kl));
-        __builtin_amdgcn_global_load_lds(
-            (const void *)(in + off + 16u * gl[q & 3]),
-            (__attribute__((address_space(3))) void *)(lds3 + 64 * q), 16, 0, 0);
+        lds_dma16_s(in + off, 16u * gl[q & 3], (lds_void *)(lds3 + 64 * q));
       }
     }
   } else {
@@ -217,9 +210,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
         rec_base = in + (rec0 + r) * in_stride;
       }
       if (s < (uint32_t)IN_SLOTS && r < nv)
-        __builtin_amdgcn_global_load_lds(
-            (const void *)(rec_base + 16u * p),
-            (__attribute__((address_space(3))) void *)(lds3 + 64 * q), 16, 0, 0);
+        lds_dma16_v(rec_base + 16u * p, (lds_void *)(lds3 + 64 * q));
     }
   }
 }
@@ -237,7 +228,11 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
 // and fix-up kernels restore or zero the record if its tag fails).
 // ABL (ablation, tools/ubench only; the product uses 0): 1 = no HBM traffic
 // (compute on whatever the LDS holds), 2 = no Poly1305 work.
-template <bool DECRYPT, int L, bool CONTIG, int MODE = kTileUniform, int ABL = 0>
+// NBUF = 2: two LDS tile buffers -- tile t+1's DMA is issued before tile t's
+// compute (instead of after it), so it lands during the compute; the wave
+// then waits only for it (a counted vmcnt lets tile t-1's stores stay in
+// flight).  Twice the LDS: 33 KB per wave at L = 1024, one wave per SIMD.
+template <bool DECRYPT, int L, bool CONTIG, int MODE = kTileUniform, int ABL = 0, int NBUF = 1>
 __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
   using C = TileCfg<L>;
   constexpr bool KEYED = MODE != kTileUniform;
@@ -247,7 +242,8 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
   constexpr int NOUT = (OUT_SLOTS + 63) / 64;          // store instructions
   static_assert(!(CONTIG && (MODE == kTileDesc || SEG)), "descriptor tiles are strided");
   static_assert(!SEG || L == 1024, "segments are 1 KiB");
-  __shared__ uint4 lds[C::NSLOT];
+  static_assert(NBUF == 1 || NBUF == 2, "one or two tile buffers");
+  __shared__ uint4 lds[NBUF * C::NSLOT];
   const uint32_t lane = threadIdx.x;
   const uint8_t *in = a.in;
   uint8_t *out = a.out;
@@ -368,15 +364,31 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
   }
   (void)own_cb;
 
+  bool prev_all = false;  // the previous tile issued all NOUT of its stores
 #pragma unroll 1
   for (int t = 0; t < C::G; ++t) {
     const uint64_t rec0 = super0 + (uint64_t)t * C::RPT;
     if (rec0 >= nrec) break;
     const uint32_t nv = (nrec - rec0) < (uint64_t)C::RPT ? (uint32_t)(nrec - rec0) : C::RPT;
+    uint4 *lb = lds + ((NBUF == 2 && (t & 1)) ? C::NSLOT : 0);  // this tile's buffer
 
-    // this tile's DMA (and the previous tile's stores) must have landed
-    wait_vmem();
+    // this tile's DMA must have landed.  NBUF = 2: it is older than the
+    // previous tile's NOUT stores, which may stay in flight (vmcnt counts
+    // loads, stores and LDS-DMA together, in issue order); whenever fewer
+    // were issued (partial tile, failed records), wait for everything.
+    if (NBUF == 2 && prev_all) wait_vmcnt<NOUT>();
+    else wait_vmem();
     wave_lds_fence();
+    if (NBUF == 2 && t + 1 < C::G) {  // the next tile's DMA now, into the other buffer
+      const uint64_t nrec0 = rec0 + C::RPT;
+      if (nrec0 < nrec) {
+        const uint64_t left = nrec - nrec0;
+        tile_load<L, DECRYPT, CONTIG, MODE, ABL>(
+            NOISE_LDS3(lds + ((t & 1) ? 0 : C::NSLOT)), in, a.in_stride, nrec0,
+            left < (uint64_t)C::RPT ? (uint32_t)left : C::RPT, lane, gl,
+            (uint32_t)(t + 1) * C::RPT, own_in_lo, own_in_hi);
+      }
+    }
 
     // ---- per-lane record work -------------------------------------------
     const uint32_t src = (uint32_t)t * C::RPT + rho;  // key lane of my record
@@ -422,13 +434,13 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint32_t slot = swz(rho * C::SPR + 4u * c + q);
-        const uint4 v = lds[slot];
+        const uint4 v = lb[slot];
         uint4 o;
         o.x = v.x ^ ks[4 * q + 0];
         o.y = v.y ^ ks[4 * q + 1];
         o.z = v.z ^ ks[4 * q + 2];
         o.w = v.w ^ ks[4 * q + 3];
-        lds[slot] = o;
+        lb[slot] = o;
         if (ABL == 2) { p.h0 ^= o.x ^ v.y; p.h1 ^= o.z ^ v.w; }
         else if (DECRYPT) poly_block(p, v.x, v.y, v.z, v.w);
         else poly_block(p, o.x, o.y, o.z, o.w);
@@ -489,7 +501,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     const bool rec_inplace = MODE == kTileDesc ? __shfl((int)own_inplace, src) != 0 : false;
     if (SEG) {
     } else if (DECRYPT) {
-      const uint4 want = lds[C::REC_SLOTS + rho];
+      const uint4 want = lb[C::REC_SLOTS + rho];
       const uint32_t diff = (want.x ^ tag[0]) | (want.y ^ tag[1]) |
                             (want.z ^ tag[2]) | (want.w ^ tag[3]);
       fail_mask |= __ballot(j == 0 && diff != 0u);
@@ -498,7 +510,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
         a.status[si] = bad_key ? 2u : (diff ? 1u : 0u);
       }
     } else if (j == 0) {
-      lds[C::REC_SLOTS + rho] = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+      lb[C::REC_SLOTS + rho] = make_uint4(tag[0], tag[1], tag[2], tag[3]);
     }
     // kTileDesc: a failed in-place record is kept, a failed copy is zeroed
     const uint64_t inpl_mask = MODE == kTileDesc ? __ballot(j == 0 && rec_inplace) : 0ull;
@@ -516,7 +528,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
       if (CONTIG && DECRYPT) slot = 64u * q + gl[q & 3];  // == swz(g)
       else slot = pc < (uint32_t)C::SPR ? swz(r * C::SPR + pc) : C::REC_SLOTS + r;
       st[q] = (OUT_SLOTS % 64 == 0 || g < (uint32_t)OUT_SLOTS) && (full || r < nv);
-      ov[q] = lds[slot < (uint32_t)C::NSLOT ? slot : 0u];
+      ov[q] = lb[slot < (uint32_t)C::NSLOT ? slot : 0u];
       if ((DECRYPT || KEYED) && fail_mask != 0 && ((fail_mask >> (r * C::G)) & 1u)) {
         // failed tag (decrypt): keep an in-place record, zero a copy;
         // invalid key index: write nothing
@@ -530,8 +542,8 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     wait_lds();  // LDS reads done
     wave_lds_fence();
 
-    // ---- next tile's DMA, then this tile's stores: both in flight at once
-    if (t + 1 < C::G) {
+    // ---- NBUF = 1: next tile's DMA, then this tile's stores, both in flight
+    if (NBUF == 1 && t + 1 < C::G) {
       const uint64_t nrec0 = rec0 + C::RPT;
       if (nrec0 < nrec) {
         const uint64_t left = nrec - nrec0;
@@ -564,6 +576,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
       }
       if (store) store16<true>(dst, ov[q], 16);
     }
+    prev_all = ABL == 0 && full && fail_mask == 0;
   }
   }  // super-tiles (one iteration unless the grid is capped: kTileDesc)
 }

@@ -13,7 +13,8 @@ import re
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", "..", ".."))
 PKG = os.path.join(ROOT, "noise-cpp_amd")
-LIB_PATH = os.path.join(PKG, "lib", "libnoise_amd.so")
+# NOISE_AMD_LIB: load another build of the library (A/B tuning runs only)
+LIB_PATH = os.environ.get("NOISE_AMD_LIB") or os.path.join(PKG, "lib", "libnoise_amd.so")
 HEADER = os.path.join(ROOT, "include", "noise_gpu.h")
 
 OK, E_NONCE, E_MAC, E_ARG, E_HIP, E_NODEV = 0, 1, 2, 3, 4, 5

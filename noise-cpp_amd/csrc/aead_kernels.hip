@@ -10,8 +10,6 @@
 //
 // One lane = one record (chachapoly_device.hpp).  Launch: 256-thread
 // workgroups, one record per thread; the grid covers nrec.
-#include <cstdlib>
-
 #include "chachapoly_device.hpp"
 #include "launchers.hpp"
 #include "tile_kernel.hpp"
@@ -79,15 +77,6 @@ __global__ __launch_bounds__(kBlock) void k_fill_synthetic_bytes(
                      (8 * (b & 7)));
 }
 
-// tile buffers of the uniform 1 KiB kernel (NOISE_TILE_NBUF=1|2, tuning)
-static int tile_nbuf() {
-  static const int n = [] {
-    const char *e = getenv("NOISE_TILE_NBUF");
-    return e && e[0] == '2' ? 2 : 1;
-  }();
-  return n;
-}
-
 static inline dim3 grid_for(uint64_t n) {
   return dim3((unsigned)((n + kBlock - 1) / kBlock));
 }
@@ -122,10 +111,7 @@ hipError_t launch_aead_uniform(bool decrypt, const uint32_t key[8],
     const bool contig = decrypt ? (in_stride == (uint64_t)len + 16 && out_stride == len)
                                 : (in_stride == len && out_stride == (uint64_t)len + 16);
 #define NOISE_TILE_LAUNCH(DEC, LEN, CONTIG)                                    \
-    if (LEN == 1024 && CONTIG && tile_nbuf() == 2)                             \
-      hipLaunchKernelGGL((k_aead_tile<DEC, LEN, CONTIG, kTileUniform, 0, 2>), gt, bt, 0, stream, ta); \
-    else                                                                       \
-      hipLaunchKernelGGL((k_aead_tile<DEC, LEN, CONTIG>), gt, bt, 0, stream, ta)
+    hipLaunchKernelGGL((k_aead_tile<DEC, LEN, CONTIG>), gt, bt, 0, stream, ta)
 #define NOISE_TILE_CASE(LEN)                                                   \
     case LEN:                                                                  \
       if (decrypt) {                                                           \

@@ -34,17 +34,22 @@
 
 namespace noise_amd {
 
-template <int L>
+// SPAN: bytes of a record per lane (256: 4 ChaCha blocks / 16 Poly1305
+// blocks per lane; 128 halves the tile: twice the lanes per record)
+template <int L, int SPAN = 256>
 struct TileCfg {
-  static constexpr int G = L >= 256 ? L / 256 : 1;  // lanes per record
+  static constexpr int G = L >= SPAN ? L / SPAN : 1;  // lanes per record
   static constexpr int RPT = 64 / G;                // records per tile
   static constexpr int CPL = (L / 64) / G;          // 64-B chunks per lane
+  static constexpr int BPL = 4 * CPL;               // Poly1305 blocks per lane
   static constexpr int SPR = L / 16;                // 16-B slots per record
   static constexpr int REC_SLOTS = RPT * SPR;
   static constexpr int NSLOT = REC_SLOTS + RPT;     // + one tag slot per record
   static constexpr int LOG2G = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3
                               : G == 16 ? 4 : G == 32 ? 5 : 6;
-  static_assert(L % 64 == 0 && 64 % G == 0 && (L < 256 || L % 256 == 0), "tile shape");
+  static constexpr int LOG2BPL = BPL == 4 ? 2 : BPL == 8 ? 3 : BPL == 16 ? 4 : 5;
+  static_assert(L % 64 == 0 && 64 % G == 0 && (L < SPAN || L % SPAN == 0), "tile shape");
+  static_assert(G == 1 || BPL == 8 || BPL == 16, "span of 128 or 256 bytes");
 };
 
 // slot <-> piece involution inside each aligned 16-slot group
@@ -143,14 +148,14 @@ __device__ __forceinline__ void desc_class_range(const TileArgs &a,
   n = a.counts[a.cls];
 }
 
-template <int L, bool DECRYPT, bool CONTIG, int MODE, int ABL>
+template <int L, bool DECRYPT, bool CONTIG, int MODE, int ABL, int SPAN>
 __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
                                           uint64_t in_stride, uint64_t rec0,
                                           uint32_t nv, uint32_t lane,
                                           const uint32_t gl[4],
                                           uint32_t t_rpt, uint32_t own_in_lo,
                                           uint32_t own_in_hi) {
-  using C = TileCfg<L>;
+  using C = TileCfg<L, SPAN>;
   if (ABL == 1) return;
   constexpr bool TAGGED_IN = DECRYPT && MODE != kTileSeg;  // ct || tag pieces
   constexpr int IN_SLOTS = TAGGED_IN ? C::NSLOT : C::REC_SLOTS;
@@ -232,16 +237,17 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
 // compute (instead of after it), so it lands during the compute; the wave
 // then waits only for it (a counted vmcnt lets tile t-1's stores stay in
 // flight).  Twice the LDS: 33 KB per wave at L = 1024, one wave per SIMD.
-template <bool DECRYPT, int L, bool CONTIG, int MODE = kTileUniform, int ABL = 0, int NBUF = 1>
+template <bool DECRYPT, int L, bool CONTIG, int MODE = kTileUniform, int ABL = 0, int NBUF = 1,
+          int SPAN = 256>
 __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
-  using C = TileCfg<L>;
+  using C = TileCfg<L, SPAN>;
   constexpr bool KEYED = MODE != kTileUniform;
   constexpr bool SEG = MODE == kTileSeg;
   constexpr int OPR = (DECRYPT || SEG) ? C::SPR : C::SPR + 1;  // out pieces / record
   constexpr int OUT_SLOTS = C::RPT * OPR;
   constexpr int NOUT = (OUT_SLOTS + 63) / 64;          // store instructions
   static_assert(!(CONTIG && (MODE == kTileDesc || SEG)), "descriptor tiles are strided");
-  static_assert(!SEG || L == 1024, "segments are 1 KiB");
+  static_assert(!SEG || (L == 1024 && SPAN == 256), "segments are 1 KiB, 256 B per lane");
   static_assert(NBUF == 1 || NBUF == 2, "one or two tile buffers");
   __shared__ uint4 lds[NBUF * C::NSLOT];
   const uint32_t lane = threadIdx.x;
@@ -298,7 +304,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     own_nlo = (uint32_t)n;
     own_nhi = (uint32_t)(n >> 32);
     const uint64_t left = nrec - super0;
-    tile_load<L, DECRYPT, CONTIG, MODE, ABL>(
+    tile_load<L, DECRYPT, CONTIG, MODE, ABL, SPAN>(
         NOISE_LDS3(lds), in, a.in_stride, super0,
         left < (uint64_t)C::RPT ? (uint32_t)left : C::RPT, lane, gl, 0u,
         own_in_lo, own_in_hi);
@@ -339,7 +345,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     // the first tile's DMA goes out before the key pass and lands meanwhile
     {
       const uint64_t left = nrec - super0;
-      tile_load<L, DECRYPT, CONTIG, MODE, ABL>(
+      tile_load<L, DECRYPT, CONTIG, MODE, ABL, SPAN>(
           NOISE_LDS3(lds), in, a.in_stride, super0,
           left < (uint64_t)C::RPT ? (uint32_t)left : C::RPT, lane, gl, 0u,
           own_in_lo, own_in_hi);
@@ -351,12 +357,10 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     kr[2] = otk[2] & 0x0ffffffcu;
     kr[3] = otk[3] & 0x0ffffffcu;
     kss[0] = otk[4]; kss[1] = otk[5]; kss[2] = otk[6]; kss[3] = otk[7];
-    if (C::G > 1) {
-      const F26 r1 = to26(kr[0], kr[1], kr[2], kr[3], 0u);
-      F26 x = mul26(r1, r1);  // r^2
-      x = mul26(x, x);        // r^4
-      x = mul26(x, x);        // r^8
-      x = mul26(x, x);        // r^16
+    if (C::G > 1) {  // r^BPL by squaring (BPL = 8 or 16)
+      F26 x = to26(kr[0], kr[1], kr[2], kr[3], 0u);
+#pragma unroll
+      for (int b = 0; b < C::LOG2BPL; ++b) x = mul26(x, x);
       pw[0] = x;
 #pragma unroll
       for (int b = 1; b < C::LOG2G; ++b) pw[b] = mul26(pw[b - 1], pw[b - 1]);
@@ -383,7 +387,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
       const uint64_t nrec0 = rec0 + C::RPT;
       if (nrec0 < nrec) {
         const uint64_t left = nrec - nrec0;
-        tile_load<L, DECRYPT, CONTIG, MODE, ABL>(
+        tile_load<L, DECRYPT, CONTIG, MODE, ABL, SPAN>(
             NOISE_LDS3(lds + ((t & 1) ? 0 : C::NSLOT)), in, a.in_stride, nrec0,
             left < (uint64_t)C::RPT ? (uint32_t)left : C::RPT, lane, gl,
             (uint32_t)(t + 1) * C::RPT, own_in_lo, own_in_hi);
@@ -451,7 +455,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
       }
     }
     if (C::G > 1) {
-      // acc_j * r^(16 (G-1-j)), then sum over the record's G lanes
+      // acc_j * r^(BPL (G-1-j)), then sum over the record's G lanes
       F26 h = to26(p.h0, p.h1, p.h2, p.h3, p.h4);
       const uint32_t m = C::G - 1 - j;
 #pragma unroll
@@ -547,7 +551,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
       const uint64_t nrec0 = rec0 + C::RPT;
       if (nrec0 < nrec) {
         const uint64_t left = nrec - nrec0;
-        tile_load<L, DECRYPT, CONTIG, MODE, ABL>(
+        tile_load<L, DECRYPT, CONTIG, MODE, ABL, SPAN>(
             NOISE_LDS3(lds), in, a.in_stride, nrec0,
             left < (uint64_t)C::RPT ? (uint32_t)left : C::RPT, lane, gl,
             (uint32_t)(t + 1) * C::RPT, own_in_lo, own_in_hi);

@@ -111,10 +111,14 @@ int noise_gpu_decrypt_uniform(const uint8_t h_key[32], uint64_t nonce0,
  * decrypt status NOISE_GPU_REC_BAD_KEY).
  * Batches of >= 2048 records are load-balanced on the device, stream-ordered
  * (no host synchronisation): records are sorted by class and each class
- * runs its own kernel -- 16-byte aligned AD-free records of 64..16384 bytes
- * (powers of two and 192) on the LDS-staged tile kernel, aligned AD-free
- * records longer than 16 KiB one wavefront per record, everything else one
- * lane per record.  Scratch comes from a per-device stream-ordered pool. */
+ * runs its own kernel -- 16-byte aligned AD-free records of 64, 128, 192,
+ * 256 and 512 bytes on the LDS-staged tile kernel; aligned AD-free records of
+ * 1024..65535 bytes (any length) cut into 1 KiB segments that ONE tile-kernel
+ * launch processes, plus a tail kernel and a per-record finalize (tag);
+ * everything else one lane per record.  Decrypt of a segmented record writes
+ * plaintext before its tag is checked and restores (in place) or zeroes
+ * (copy) it when the tag fails, so the final buffer contents follow the rules
+ * above.  Scratch is a grow-only device buffer per (device, stream). */
 int noise_gpu_encrypt_records(const uint8_t *d_keys, uint32_t nkeys,
                               const noise_gpu_record *d_recs, uint64_t nrec,
                               const uint8_t *d_in, uint8_t *d_out,

@@ -359,6 +359,30 @@ def test_cipherstate_cpp_surface():
     assert "PASSED" in r.stdout
 
 
+def test_handshake_vectors():
+    """Host HandshakeState (host/handshake.cpp) over the reference's 110
+    Noise_*_25519_ChaChaPoly_BLAKE2b vectors (tests/golden/handshake_vectors.tsv,
+    extracted from /root/reference/tests/vectors): every handshake message
+    byte-exact, the handshake hash, and the transport records through the
+    GPU-backed CipherState pair that split() returns."""
+    exe = os.path.join(noise_amd.ROOT, "noise-cpp_amd", "bin", "handshake_test")
+    r = subprocess.run([exe, "vectors", os.path.join(noise_amd.ROOT, "tests", "golden",
+                                                     "handshake_vectors.tsv")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "vectors 110, failed 0" in r.stdout, r.stdout
+
+
+def test_xx_loopback_config1_shape():
+    """BASELINE config 1 shape: XX loopback handshake with fresh keys, then
+    1000 x 1 KiB transport records each way (examples/Noise_XX_*.cpp:26-71)."""
+    exe = os.path.join(noise_amd.ROOT, "noise-cpp_amd", "bin", "handshake_test")
+    r = subprocess.run([exe, "loopback", "1000", "1024"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert '"ok": true' in r.stdout
+
+
 def _sessions_case(rng, nkeys, per, length):
     keys = [rng.randbytes(32) for _ in range(nkeys)]
     nrec = nkeys * per

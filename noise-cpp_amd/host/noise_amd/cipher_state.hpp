@@ -66,6 +66,9 @@ public:
   // ---- batch extensions (not in the reference surface) -----------------
   // Current nonce (the reference keeps n private and has no getter).
   [[nodiscard]] std::uint64_t nonce() const { return n; }
+  // The key, for handing a session to a device-side batch (the key table of
+  // noise_gpu_*_records / noise::transport::Batcher).
+  [[nodiscard]] const std::array<std::uint8_t, 32> &key_material() const { return k; }
 
   // Encrypt every message in order with nonces n, n+1, ... exactly as a
   // loop of encrypt_with_ad would (each grows by 16).  Stops with

@@ -383,6 +383,19 @@ def test_xx_loopback_config1_shape():
     assert '"ok": true' in r.stdout
 
 
+@pytest.mark.parametrize("sessions,messages,seed", [(100, 1000, 1), (300, 5000, 2)])
+def test_transport_batcher(sessions, messages, seed):
+    """noise::transport (host/transport.cpp): many sessions' messages in one
+    descriptor batch each way (below and above the 2048-record classifier
+    threshold), ciphertexts vs the CPU oracle, BE16 framing through a chunked
+    Deframer, tampered records rejected, per-session nonce accounting."""
+    exe = os.path.join(noise_amd.ROOT, "noise-cpp_amd", "bin", "transport_test")
+    r = subprocess.run([exe, str(sessions), str(messages), str(seed)], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "ok (0 failures)" in r.stdout
+
+
 def _sessions_case(rng, nkeys, per, length):
     keys = [rng.randbytes(32) for _ in range(nkeys)]
     nrec = nkeys * per

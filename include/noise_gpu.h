@@ -158,6 +158,16 @@ int noise_gpu_decrypt_sessions(const uint8_t *d_keys, uint32_t nkeys,
  * k <- ENCRYPT(k, 2^64-2, empty, 0^32)[0..32)   (noise.cpp:429-439). */
 int noise_gpu_rekey_keys(uint8_t *d_keys, uint64_t nkeys, void *stream);
 
+/* ---- batched X25519 (mass handshakes) -----------------------------------
+ * d_out[i] = X25519(d_scalars[i], d_points[i]) for i < n: 32-byte little-
+ * endian scalars (clamped as RFC 7748 §5), u-coordinates and results, 16-byte
+ * aligned arrays of n x 32 bytes.  d_points == NULL: the base point u = 9
+ * (public keys).  Replaces, for many sessions at once, noise::dh /
+ * generate_keypair -> crypto_x25519 / crypto_x25519_public_key
+ * (noise.cpp:164-177, monocypher.c:1546-1563).  Asynchronous on stream. */
+int noise_gpu_x25519(const uint8_t *d_scalars, const uint8_t *d_points,
+                     uint8_t *d_out, uint64_t n, void *stream);
+
 /* ---- host-buffer entry points (synchronous) ----------------------------
  * Used by the CipherState shim for single records (encrypt_with_ad /
  * decrypt_with_ad / rekey).  They stage through pinned host memory and a

@@ -35,6 +35,9 @@ hipError_t launch_aead_sessions(bool decrypt, const uint8_t *keys,
 
 hipError_t launch_rekey(uint8_t *keys, uint64_t nkeys, hipStream_t stream);
 
+hipError_t launch_x25519(const uint8_t *scalars, const uint8_t *points,
+                         uint8_t *out, uint64_t n, hipStream_t stream);
+
 hipError_t launch_fill_synthetic(uint8_t *dst, uint64_t offset,
                                  uint64_t nbytes, uint64_t seed,
                                  hipStream_t stream);

@@ -273,6 +273,19 @@ int noise_gpu_rekey_keys(uint8_t *d_keys, uint64_t nkeys, void *stream) {
   return NOISE_GPU_OK;
 }
 
+int noise_gpu_x25519(const uint8_t *d_scalars, const uint8_t *d_points,
+                     uint8_t *d_out, uint64_t n, void *stream) {
+  if (n == 0) return NOISE_GPU_OK;
+  if (!d_scalars || !d_out) return arg_fail("null scalars / output");
+  if (((reinterpret_cast<uintptr_t>(d_scalars) | reinterpret_cast<uintptr_t>(d_points) |
+        reinterpret_cast<uintptr_t>(d_out)) & 15u) != 0)
+    return arg_fail("X25519 arrays must be 16-byte aligned");
+  int rc = check_device();
+  if (rc) return rc;
+  HIP_TRY(noise_amd::launch_x25519(d_scalars, d_points, d_out, n, (hipStream_t)stream));
+  return NOISE_GPU_OK;
+}
+
 int noise_gpu_fill_synthetic(uint8_t *d_dst, uint64_t offset, uint64_t nbytes,
                              uint64_t seed, void *stream) {
   if (nbytes == 0) return NOISE_GPU_OK;

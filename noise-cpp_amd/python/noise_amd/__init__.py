@@ -81,6 +81,7 @@ def load(path=LIB_PATH):
         "noise_gpu_encrypt_records": (ctypes.c_int, [u8p, u32, u8p, u64, u8p, u8p, u8p, vp]),
         "noise_gpu_decrypt_records": (ctypes.c_int, [u8p, u32, u8p, u64, u8p, u8p, u8p, u8p, vp]),
         "noise_gpu_rekey_keys": (ctypes.c_int, [u8p, u64, vp]),
+        "noise_gpu_x25519": (ctypes.c_int, [u8p, u8p, u8p, u64, vp]),
         "noise_gpu_encrypt_sessions": (ctypes.c_int, [u8p, u32, u8p, u8p, u8p, u64, u8p, u64, u32,
                                                       u64, vp]),
         "noise_gpu_decrypt_sessions": (ctypes.c_int, [u8p, u32, u8p, u8p, u8p, u64, u8p, u64, u32,
@@ -183,6 +184,12 @@ def decrypt_sessions(d_keys, nkeys, d_key_idx, d_nonces, d_in, in_stride, d_out,
 
 def rekey_keys(d_keys, nkeys, stream=None):
     _check(load().noise_gpu_rekey_keys(_ptr(d_keys), nkeys, _stream(stream)), "noise_gpu_rekey_keys")
+
+
+def x25519(d_scalars, d_points, d_out, n, stream=None):
+    """d_out[i] = X25519(d_scalars[i], d_points[i] or 9): n x 32-byte device arrays."""
+    _check(load().noise_gpu_x25519(_ptr(d_scalars), _ptr(d_points) if d_points is not None else None,
+                                   _ptr(d_out), n, _stream(stream)), "noise_gpu_x25519")
 
 
 def fill_synthetic(d_dst, nbytes, seed, offset=0, stream=None, dst_offset=0):

@@ -104,3 +104,43 @@ double ref_batch_uniform(int decrypt, const uint8_t key[32], uint64_t n0,
   if (fails) *fails = f;
   return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+/* The reference's X25519 (monocypher.c:1546-1563, called by noise::dh,
+ * noise.cpp:172-177): one result, for parity, and a timed loop on `threads`
+ * host threads for the CPU baseline of tools/bench_x25519.py.  Returns the
+ * wall seconds of n scalar multiplications (chained: each output is the
+ * next point, so nothing is skipped). */
+void ref_x25519(uint8_t out[32], const uint8_t scalar[32], const uint8_t point[32]) {
+  crypto_x25519(out, scalar, point);
+}
+
+struct xjob {
+  uint8_t k[32], u[32];
+  long n;
+};
+
+static void *run_x(void *arg) {
+  struct xjob *j = (struct xjob *)arg;
+  for (long i = 0; i < j->n; ++i) crypto_x25519(j->u, j->k, j->u);
+  return NULL;
+}
+
+double ref_x25519_bench(long n, int threads) {
+  if (threads < 1) threads = 1;
+  if (threads > 64) threads = 64;
+  pthread_t th[64];
+  struct xjob jobs[64];
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  for (int t = 0; t < threads; ++t) {
+    for (int b = 0; b < 32; ++b) {
+      jobs[t].k[b] = (uint8_t)(7 * b + t + 1);
+      jobs[t].u[b] = (uint8_t)(b == 0 ? 9 : 0);
+    }
+    jobs[t].n = n / threads;
+    pthread_create(&th[t], NULL, run_x, &jobs[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

@@ -533,14 +533,22 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
       else slot = pc < (uint32_t)C::SPR ? swz(r * C::SPR + pc) : C::REC_SLOTS + r;
       st[q] = (OUT_SLOTS % 64 == 0 || g < (uint32_t)OUT_SLOTS) && (full || r < nv);
       ov[q] = lb[slot < (uint32_t)C::NSLOT ? slot : 0u];
-      if ((DECRYPT || KEYED) && fail_mask != 0 && ((fail_mask >> (r * C::G)) & 1u)) {
-        // failed tag (decrypt): keep an in-place record, zero a copy;
-        // invalid key index: write nothing
-        const bool bad_key_rec = KEYED && ((badk_mask >> (r * C::G)) & 1u);
-        const bool inpl = MODE == kTileDesc ? ((inpl_mask >> (r * C::G)) & 1u) != 0
-                                            : a.in_place != 0;
-        st[q] = st[q] && DECRYPT && !inpl && !bad_key_rec;
-        ov[q] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    // Records that must not be output as computed (rare; a separate,
+    // wave-uniform branch so the common path carries none of this):
+    // failed tag (decrypt): keep an in-place record, zero a copy; invalid key
+    // index: write nothing.
+    if ((DECRYPT || KEYED) && fail_mask != 0) {
+#pragma unroll
+      for (int q = 0; q < NOUT; ++q) {
+        const uint32_t r = (64u * q + lane) / OPR;
+        if ((fail_mask >> (r * C::G)) & 1u) {
+          const bool bad_key_rec = KEYED && ((badk_mask >> (r * C::G)) & 1u);
+          const bool inpl = MODE == kTileDesc ? ((inpl_mask >> (r * C::G)) & 1u) != 0
+                                              : a.in_place != 0;
+          st[q] = st[q] && DECRYPT && !inpl && !bad_key_rec;
+          ov[q] = make_uint4(0u, 0u, 0u, 0u);
+        }
       }
     }
     wait_lds();  // LDS reads done

@@ -7,7 +7,8 @@
 // One lane = one scalar multiplication.  Field elements mod 2^255-19 in ten
 // limbs of alternately 26 and 25 bits (radix 2^25.5) held in VGPRs; a field
 // product is 100 32x32->64 multiply-adds (v_mad_u64_u32) plus one carry
-// pass.  The ladder has no secret-dependent branch or address: the swap is
+// pass (a square: 55); sums and differences stay uncarried into the next
+// product.  The ladder has no secret-dependent branch or address: the swap is
 // an arithmetic mask, so all 64 lanes of a wave run the same instruction
 // stream (constant time per lane, no divergence).  Inversion by the standard
 // 254-squaring / 11-multiplication chain for p-2.
@@ -48,10 +49,13 @@ __device__ __forceinline__ void fe_reduce(Fe &h) {
   fe_carry(h, t);
 }
 
+// Sums and differences are NOT carried: every operand of the ladder's adds
+// and subs is a carried product (limbs <= 2^26 / 2^25 + small), so their
+// results stay below 2^27.6 per limb, and fe_mul / fe_sq accept that (19 * limb
+// < 2^32, every 64-bit column sum < 2^63.7).
 __device__ __forceinline__ void fe_add(Fe &h, const Fe &f, const Fe &g) {
 #pragma unroll
   for (int i = 0; i < 10; ++i) h.v[i] = f.v[i] + g.v[i];
-  fe_reduce(h);
 }
 
 // f + 2p - g (g carried: limbs <= 2^26 / 2^25 + small)
@@ -60,7 +64,6 @@ __device__ __forceinline__ void fe_sub(Fe &h, const Fe &f, const Fe &g) {
 #pragma unroll
   for (int i = 1; i < 10; ++i)
     h.v[i] = f.v[i] + ((i & 1) ? 0x3fffffeu : 0x7fffffeu) - g.v[i];  // 2^26-2 / 2^27-2
-  fe_reduce(h);
 }
 
 __device__ __forceinline__ uint64_t m64(uint32_t a, uint32_t b) { return (uint64_t)a * b; }
@@ -94,7 +97,36 @@ __device__ __forceinline__ void fe_mul(Fe &h, const Fe &F, const Fe &G) {
   fe_carry(h, t);
 }
 
-__device__ __forceinline__ void fe_sq(Fe &h, const Fe &f) { fe_mul(h, f, f); }
+// f^2 with the symmetric products merged: 55 multiply-adds instead of 100
+__device__ __forceinline__ void fe_sq(Fe &h, const Fe &F) {
+  const uint32_t *f = F.v;
+  const uint32_t f0_2 = 2 * f[0], f1_2 = 2 * f[1], f2_2 = 2 * f[2], f3_2 = 2 * f[3],
+                 f4_2 = 2 * f[4], f5_2 = 2 * f[5], f6_2 = 2 * f[6], f7_2 = 2 * f[7];
+  const uint32_t f5_38 = 38 * f[5], f6_19 = 19 * f[6], f7_38 = 38 * f[7], f8_19 = 19 * f[8],
+                 f9_38 = 38 * f[9];
+  uint64_t t[10];
+  t[0] = m64(f[0], f[0]) + m64(f1_2, f9_38) + m64(f2_2, f8_19) + m64(f3_2, f7_38) +
+         m64(f4_2, f6_19) + m64(f[5], f5_38);
+  t[1] = m64(f0_2, f[1]) + m64(f[2], f9_38) + m64(f3_2, f8_19) + m64(f[4], f7_38) +
+         m64(f5_2, f6_19);
+  t[2] = m64(f0_2, f[2]) + m64(f1_2, f[1]) + m64(f3_2, f9_38) + m64(f4_2, f8_19) +
+         m64(f5_2, f7_38) + m64(f[6], f6_19);
+  t[3] = m64(f0_2, f[3]) + m64(f1_2, f[2]) + m64(f[4], f9_38) + m64(f5_2, f8_19) +
+         m64(f[6], f7_38);
+  t[4] = m64(f0_2, f[4]) + m64(f1_2, f3_2) + m64(f[2], f[2]) + m64(f5_2, f9_38) +
+         m64(f6_2, f8_19) + m64(f[7], f7_38);
+  t[5] = m64(f0_2, f[5]) + m64(f1_2, f[4]) + m64(f2_2, f[3]) + m64(f[6], f9_38) +
+         m64(f7_2, f8_19);
+  t[6] = m64(f0_2, f[6]) + m64(f1_2, f5_2) + m64(f2_2, f[4]) + m64(f3_2, f[3]) +
+         m64(f7_2, f9_38) + m64(f[8], f8_19);
+  t[7] = m64(f0_2, f[7]) + m64(f1_2, f[6]) + m64(f2_2, f[5]) + m64(f3_2, f[4]) +
+         m64(f[8], f9_38);
+  t[8] = m64(f0_2, f[8]) + m64(f1_2, f7_2) + m64(f2_2, f[6]) + m64(f3_2, f5_2) +
+         m64(f[4], f[4]) + m64(f[9], f9_38);
+  t[9] = m64(f0_2, f[9]) + m64(f1_2, f[8]) + m64(f2_2, f[7]) + m64(f3_2, f[6]) +
+         m64(f4_2, f[5]);
+  fe_carry(h, t);
+}
 
 __device__ __forceinline__ void fe_sqn(Fe &h, const Fe &f, int n) {
   fe_sq(h, f);

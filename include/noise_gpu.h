@@ -168,6 +168,94 @@ int noise_gpu_rekey_keys(uint8_t *d_keys, uint64_t nkeys, void *stream);
 int noise_gpu_x25519(const uint8_t *d_scalars, const uint8_t *d_points,
                      uint8_t *d_out, uint64_t n, void *stream);
 
+/* ---- batched handshakes (mass handshakes) -------------------------------
+ * n sessions running the same pattern in the same role, in lockstep: every
+ * token of a message runs as one GPU kernel over all n sessions (one lane per
+ * session: X25519 ladder, BLAKE2b / HMAC / HKDF, ChaChaPoly with AD = h),
+ * session state resident in HBM.  Replaces, for many handshakes at once,
+ * noise::HandshakeState initialize / write_message / read_message / finalize
+ * (noise.h:137-173, noise.cpp:545-1100), with the spec semantics of the host
+ * noise::HandshakeState (noise_amd/handshake.hpp; suite
+ * Noise_<pattern>_25519_ChaChaPoly_BLAKE2b).  All functions are asynchronous
+ * on `stream` except create/destroy/info; arrays are device pointers.
+ *
+ * Per-session byte ranges are described by a span: session i's bytes start
+ * at base + (off ? off[i] : i * stride) and are len ? len[i] : len_all long
+ * (the length is ignored where the library determines it). */
+typedef struct noise_gpu_span {
+  uint8_t *base;
+  const uint64_t *off; /* per-session offsets, or NULL: i * stride      */
+  uint64_t stride;
+  const uint32_t *len; /* per-session lengths, or NULL: len_all         */
+  uint32_t len_all;
+  uint32_t reserved;
+} noise_gpu_span;
+
+typedef struct noise_gpu_hs noise_gpu_hs;
+
+/* key slots of noise_gpu_hs_set_key */
+#define NOISE_GPU_HS_S 0  /* local static private key (public derived)  */
+#define NOISE_GPU_HS_E 1  /* local ephemeral private key (test vectors;
+                             otherwise generated at the "e" token)       */
+#define NOISE_GPU_HS_RS 2 /* remote static public key                   */
+#define NOISE_GPU_HS_RE 3 /* remote ephemeral public key                */
+
+/* per-session status (noise_gpu_hs_status, read_message) */
+#define NOISE_GPU_HS_OK 0u
+#define NOISE_GPU_HS_BAD_MAC 1u /* a handshake AEAD tag did not verify */
+#define NOISE_GPU_HS_BAD_LEN 3u /* message shorter than its tokens, or > 65535 */
+
+typedef struct noise_gpu_hs_info {
+  uint32_t message_index; /* next message of the pattern (0-based)         */
+  uint32_t message_count;
+  int32_t my_turn;        /* 1: next call is write_message, 0: read_message */
+  int32_t finished;       /* all messages done: split() may be called     */
+  uint32_t overhead;      /* bytes of the next message besides the payload
+                             (token bytes + the payload tag if keyed)     */
+  uint32_t psk_count;     /* psks each session needs (noise_gpu_hs_set_psks) */
+} noise_gpu_hs_info;
+
+/* pattern: name as in the protocol name, with psk modifiers ("XX", "IK",
+ * "XXpsk0+psk2").  n: sessions.  Allocates n x 384 B of device state on the
+ * current device. */
+int noise_gpu_hs_create(const char *pattern, int initiator, uint64_t n,
+                        noise_gpu_hs **out);
+/* wipes the device state, then frees it (synchronises the device) */
+int noise_gpu_hs_destroy(noise_gpu_hs *hs);
+int noise_gpu_hs_info_get(const noise_gpu_hs *hs, noise_gpu_hs_info *out);
+/* Before noise_gpu_hs_start: install key slot `which` for every session from
+ * d_keys (32 bytes per session at `stride`; stride 0 = one key for all). */
+int noise_gpu_hs_set_key(noise_gpu_hs *hs, int which, const uint8_t *d_keys,
+                         uint64_t stride, void *stream);
+/* Before noise_gpu_hs_start: the psks, n x psk_count x 32 bytes (copied). */
+int noise_gpu_hs_set_psks(noise_gpu_hs *hs, const uint8_t *d_psks, void *stream);
+/* InitializeSymmetric + MixHash(prologue) + the pre-messages.  prologue may
+ * be NULL (empty prologue for every session). */
+int noise_gpu_hs_start(noise_gpu_hs *hs, const noise_gpu_span *prologue,
+                       void *stream);
+/* WriteMessage for every session: payload (NULL = empty) -> msg at msg's
+ * offsets (msg lengths ignored; each needs overhead + payload bytes);
+ * d_msg_len (may be NULL) receives the message lengths. */
+int noise_gpu_hs_write_message(noise_gpu_hs *hs, const noise_gpu_span *payload,
+                               const noise_gpu_span *msg, uint32_t *d_msg_len,
+                               void *stream);
+/* ReadMessage for every session: msg (with lengths) -> payload at payload's
+ * offsets (room for msg length - overhead bytes; may be NULL if every payload
+ * is empty).  d_payload_len (may be NULL): payload lengths; d_status (may be
+ * NULL): per-session NOISE_GPU_HS_* after this message.  A failed session
+ * stays failed: later calls skip it and split() gives it all-zero keys. */
+int noise_gpu_hs_read_message(noise_gpu_hs *hs, const noise_gpu_span *msg,
+                              const noise_gpu_span *payload,
+                              uint32_t *d_payload_len, uint8_t *d_status,
+                              void *stream);
+int noise_gpu_hs_status(const noise_gpu_hs *hs, uint8_t *d_status, void *stream);
+/* Split() of every finished session: d_k1[i] (initiator -> responder) and
+ * d_k2[i] (responder -> initiator), 32-byte key rows that the sessions /
+ * records entry points take as key tables; optionally the handshake hash
+ * (64-byte rows) and the remote static public key (32-byte rows). */
+int noise_gpu_hs_split(noise_gpu_hs *hs, uint8_t *d_k1, uint8_t *d_k2,
+                       uint8_t *d_hash, uint8_t *d_rs, void *stream);
+
 /* ---- host-buffer entry points (synchronous) ----------------------------
  * Used by the CipherState shim for single records (encrypt_with_ad /
  * decrypt_with_ad / rekey).  They stage through pinned host memory and a

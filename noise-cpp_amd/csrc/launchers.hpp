@@ -38,6 +38,61 @@ hipError_t launch_rekey(uint8_t *keys, uint64_t nkeys, hipStream_t stream);
 hipError_t launch_x25519(const uint8_t *scalars, const uint8_t *points,
                          uint8_t *out, uint64_t n, hipStream_t stream);
 
+// ---- batched handshakes (handshake_kernels.hip, handshake_batch.hip) ----
+// One session's handshake state in HBM (AoS row, 16-byte aligned words).
+struct HsSession {
+  uint32_t ck[16];      // chaining key
+  uint32_t h[16];       // handshake hash
+  uint32_t k[8];        // CipherState key (meaningful while the host's has_k)
+  uint32_t status;      // 0, or the sticky NOISE_GPU_HS_* failure code
+  uint32_t pad[7];
+  uint32_t keys[6][8];  // HsKey slots
+};
+enum HsKey : int { kHsSsk = 0, kHsSpk = 1, kHsEsk = 2, kHsEpk = 3, kHsRs = 4, kHsRe = 5 };
+struct HsWords16 { uint32_t w[16]; };
+struct HsWords8 { uint32_t w[8]; };
+// Per-session byte range: base + (off ? off[i] : i * stride) + add, length
+// len ? len[i] + len_adj : len_u.
+struct HsSpan {
+  uint8_t *base;
+  const uint64_t *off;
+  uint64_t stride;
+  const uint32_t *len;
+  uint32_t len_u;
+  int32_t len_adj;
+  uint32_t add;
+  uint32_t pad;
+};
+
+hipError_t launch_hs_init(HsSession *S, uint64_t n, const HsWords16 &h0, const HsSpan &prologue,
+                          hipStream_t st);
+hipError_t launch_hs_set_key(HsSession *S, uint64_t n, int which, const uint8_t *src,
+                             uint64_t src_stride, const HsWords8 &seed, uint32_t drbg_ctr,
+                             bool derive_pk, hipStream_t st);
+hipError_t launch_hs_bcast_key(HsSession *S, uint64_t n, int which, int count, hipStream_t st);
+hipError_t launch_hs_key_token(HsSession *S, uint64_t n, int which, int io, const HsSpan &msg,
+                               bool hash, bool key, hipStream_t st);
+hipError_t launch_hs_dh(HsSession *S, uint64_t n, int sk, int pk, hipStream_t st);
+hipError_t launch_hs_psk(HsSession *S, uint64_t n, const uint8_t *psks, uint32_t npsk,
+                         uint32_t idx, hipStream_t st);
+hipError_t launch_hs_check_len(HsSession *S, uint64_t n, const uint32_t *len, uint32_t min_len,
+                               hipStream_t st);
+hipError_t launch_hs_encrypt_hash(HsSession *S, uint64_t n, bool has_k, uint64_t nonce,
+                                  int src_key, const HsSpan &src, const HsSpan &dst,
+                                  uint32_t *out_len, hipStream_t st);
+hipError_t launch_hs_decrypt_hash(HsSession *S, uint64_t n, bool has_k, uint64_t nonce,
+                                  const HsSpan &src, int dst_key, const HsSpan &dst,
+                                  uint32_t *out_len, hipStream_t st);
+hipError_t launch_hs_split(HsSession *S, uint64_t n, uint8_t *k1, uint8_t *k2, uint8_t *hash,
+                           uint8_t *rs, hipStream_t st);
+hipError_t launch_hs_status(const HsSession *S, uint64_t n, uint8_t *out, hipStream_t st);
+hipError_t launch_hs_wipe(HsSession *S, uint64_t n, hipStream_t st);
+
+// C-ABI helpers shared by the API translation units (noise_gpu_api.hip)
+int api_hip_fail(hipError_t e, const char *what);
+int api_arg_fail(const char *msg);
+int api_check_device();
+
 hipError_t launch_fill_synthetic(uint8_t *dst, uint64_t offset,
                                  uint64_t nbytes, uint64_t seed,
                                  hipStream_t stream);

@@ -117,6 +117,12 @@ inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
 }  // namespace
 
+namespace noise_amd {
+int api_hip_fail(hipError_t e, const char *what) { return hip_fail(e, what); }
+int api_arg_fail(const char *msg) { return arg_fail(msg); }
+int api_check_device() { return check_device(); }
+}  // namespace noise_amd
+
 extern "C" {
 
 const char *noise_gpu_version(void) { return "noise-mi355x 0.1.0 gfx950"; }

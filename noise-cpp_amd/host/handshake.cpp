@@ -198,8 +198,8 @@ void HandshakeState::initialize(const HandshakeStateConfiguration &config) {
   initialize_named(pattern_name(config.pattern), config);
 }
 
-void HandshakeState::initialize_named(std::string_view pattern,
-                                      const HandshakeStateConfiguration &config) {
+namespace detail {
+PatternProgram parse_pattern(std::string_view pattern) {
   // base pattern + psk modifiers ("XXpsk0+psk2")
   std::string_view base = pattern;
   std::vector<int> psk_at;
@@ -225,25 +225,38 @@ void HandshakeState::initialize_named(std::string_view pattern,
     if (base == d.name) def = &d;
   if (!def) throw std::logic_error("unknown handshake pattern");
 
-  initiator_pre_message_pattern = parse_tokens(def->pre_i);
-  responder_pre_message_pattern = parse_tokens(def->pre_r);
-  message_patterns.clear();
+  PatternProgram prog;
+  prog.pre_i = parse_tokens(def->pre_i);
+  prog.pre_r = parse_tokens(def->pre_r);
   for (std::string_view m = def->msgs; !m.empty();) {
     std::size_t j = m.find('|');
     if (j == std::string_view::npos) j = m.size();
-    message_patterns.push_back(parse_tokens(m.substr(0, j)));
+    prog.msgs.push_back(parse_tokens(m.substr(0, j)));
     m = j < m.size() ? m.substr(j + 1) : std::string_view();
   }
   for (int n : psk_at) {  // psk0: first token of message 1; pskN: last of message N
     if (n == 0) {
-      message_patterns.front().insert(message_patterns.front().begin(), PatternToken::Psk);
+      prog.msgs.front().insert(prog.msgs.front().begin(), PatternToken::Psk);
     } else {
-      if ((std::size_t)n > message_patterns.size()) throw std::logic_error("psk modifier past the last message");
-      message_patterns[n - 1].push_back(PatternToken::Psk);
+      if ((std::size_t)n > prog.msgs.size()) throw std::logic_error("psk modifier past the last message");
+      prog.msgs[n - 1].push_back(PatternToken::Psk);
     }
   }
-  psk_mode = !psk_at.empty();
-  if (config.psks.size() != psk_at.size()) throw std::invalid_argument("psk count does not match the pattern");
+  prog.npsk = psk_at.size();
+  prog.psk_mode = !psk_at.empty();
+  prog.one_way = base == "N" || base == "K" || base == "X";
+  return prog;
+}
+}  // namespace detail
+
+void HandshakeState::initialize_named(std::string_view pattern,
+                                      const HandshakeStateConfiguration &config) {
+  const detail::PatternProgram prog = detail::parse_pattern(pattern);
+  initiator_pre_message_pattern = prog.pre_i;
+  responder_pre_message_pattern = prog.pre_r;
+  message_patterns.assign(prog.msgs.begin(), prog.msgs.end());
+  psk_mode = prog.psk_mode;
+  if (config.psks.size() != prog.npsk) throw std::invalid_argument("psk count does not match the pattern");
   psks.assign(config.psks.begin(), config.psks.end());
   for (const auto &p : psks)
     if (p.size() != 32) throw std::invalid_argument("psk must be 32 bytes");

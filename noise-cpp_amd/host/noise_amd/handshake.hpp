@@ -53,6 +53,21 @@ enum class HandshakePattern : std::uint8_t {
 // pattern name as it appears in the protocol name ("XXpsk3")
 std::string_view pattern_name(HandshakePattern p);
 
+namespace detail {
+// A pattern name with psk modifiers ("XXpsk0+psk2") parsed into its
+// pre-messages and per-message token lists (rev34 §7, §9; the reference's
+// table is noise.cpp:594-818).  Shared by HandshakeState and the batched GPU
+// handshake (noise_gpu_hs_*).  Throws std::logic_error for unknown names.
+struct PatternProgram {
+  std::vector<PatternToken> pre_i, pre_r;
+  std::vector<std::vector<PatternToken>> msgs;
+  std::size_t npsk = 0;
+  bool psk_mode = false;
+  bool one_way = false;  // N, K, X and their psk variants: initiator writes all
+};
+PatternProgram parse_pattern(std::string_view name);
+}  // namespace detail
+
 struct KeyPair {
   std::array<std::uint8_t, 32> sk;
   std::array<std::uint8_t, 32> pk;

@@ -44,6 +44,23 @@ def record_dtype():
     return RECORD_DTYPE
 
 
+class Span(ctypes.Structure):
+    """noise_gpu_span (include/noise_gpu.h): per-session byte ranges."""
+    _fields_ = [("base", ctypes.c_void_p), ("off", ctypes.c_void_p), ("stride", ctypes.c_uint64),
+                ("len", ctypes.c_void_p), ("len_all", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+class HsInfo(ctypes.Structure):
+    """noise_gpu_hs_info (include/noise_gpu.h)."""
+    _fields_ = [("message_index", ctypes.c_uint32), ("message_count", ctypes.c_uint32),
+                ("my_turn", ctypes.c_int32), ("finished", ctypes.c_int32),
+                ("overhead", ctypes.c_uint32), ("psk_count", ctypes.c_uint32)]
+
+
+HS_S, HS_E, HS_RS, HS_RE = 0, 1, 2, 3
+HS_OK, HS_BAD_MAC, HS_BAD_LEN = 0, 1, 3
+
+
 class NoiseGpuError(RuntimeError):
     def __init__(self, code, what):
         super().__init__("%s (status %d): %s" % (what, code, _lib.noise_gpu_last_error().decode()
@@ -101,6 +118,19 @@ def load(path=LIB_PATH):
                                                           u32, u8p, u64,
                                                           ctypes.POINTER(ctypes.c_double)]),
         "noise_gpu_fill_synthetic": (ctypes.c_int, [u8p, u64, u64, u64, vp]),
+        "noise_gpu_hs_create": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, u64,
+                                               ctypes.POINTER(ctypes.c_void_p)]),
+        "noise_gpu_hs_destroy": (ctypes.c_int, [vp]),
+        "noise_gpu_hs_info_get": (ctypes.c_int, [vp, ctypes.POINTER(HsInfo)]),
+        "noise_gpu_hs_set_key": (ctypes.c_int, [vp, ctypes.c_int, u8p, u64, vp]),
+        "noise_gpu_hs_set_psks": (ctypes.c_int, [vp, u8p, vp]),
+        "noise_gpu_hs_start": (ctypes.c_int, [vp, ctypes.POINTER(Span), vp]),
+        "noise_gpu_hs_write_message": (ctypes.c_int, [vp, ctypes.POINTER(Span), ctypes.POINTER(Span),
+                                                      u8p, vp]),
+        "noise_gpu_hs_read_message": (ctypes.c_int, [vp, ctypes.POINTER(Span), ctypes.POINTER(Span),
+                                                     u8p, u8p, vp]),
+        "noise_gpu_hs_status": (ctypes.c_int, [vp, u8p, vp]),
+        "noise_gpu_hs_split": (ctypes.c_int, [vp, u8p, u8p, u8p, u8p, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -196,6 +226,71 @@ def fill_synthetic(d_dst, nbytes, seed, offset=0, stream=None, dst_offset=0):
     rc = load().noise_gpu_fill_synthetic(ctypes.c_void_p(d_dst.data_ptr() + dst_offset), offset,
                                          nbytes, seed, _stream(stream))
     _check(rc, "noise_gpu_fill_synthetic")
+
+
+def span(base, stride=0, length=0, off=None, lens=None):
+    """A noise_gpu_span over torch device tensors (base: uint8, off: int64
+    offsets, lens: int32 lengths; None = uniform stride / length)."""
+    return Span(base.data_ptr(), None if off is None else off.data_ptr(), stride,
+                None if lens is None else lens.data_ptr(), length, 0)
+
+
+class HandshakeBatch:
+    """n sessions of one handshake pattern in one role on the GPU
+    (noise_gpu_hs_*): the batched form of noise::HandshakeState."""
+
+    def __init__(self, pattern, initiator, n):
+        self.lib, self.n = load(), n
+        h = ctypes.c_void_p()
+        _check(self.lib.noise_gpu_hs_create(pattern.encode(), 1 if initiator else 0, n,
+                                            ctypes.byref(h)), "noise_gpu_hs_create")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            _check(self.lib.noise_gpu_hs_destroy(self.h), "noise_gpu_hs_destroy")
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self):
+        i = HsInfo()
+        _check(self.lib.noise_gpu_hs_info_get(self.h, ctypes.byref(i)), "noise_gpu_hs_info_get")
+        return i
+
+    def set_key(self, which, d_keys, stride=32, stream=None):
+        _check(self.lib.noise_gpu_hs_set_key(self.h, which, _ptr(d_keys), stride, _stream(stream)),
+               "noise_gpu_hs_set_key")
+
+    def set_psks(self, d_psks, stream=None):
+        _check(self.lib.noise_gpu_hs_set_psks(self.h, _ptr(d_psks), _stream(stream)),
+               "noise_gpu_hs_set_psks")
+
+    def start(self, prologue=None, stream=None):
+        _check(self.lib.noise_gpu_hs_start(self.h, ctypes.byref(prologue) if prologue else None,
+                                           _stream(stream)), "noise_gpu_hs_start")
+
+    def write_message(self, msg, payload=None, d_msg_len=None, stream=None):
+        _check(self.lib.noise_gpu_hs_write_message(
+            self.h, ctypes.byref(payload) if payload else None, ctypes.byref(msg), _ptr(d_msg_len),
+            _stream(stream)), "noise_gpu_hs_write_message")
+
+    def read_message(self, msg, payload=None, d_payload_len=None, d_status=None, stream=None):
+        _check(self.lib.noise_gpu_hs_read_message(
+            self.h, ctypes.byref(msg), ctypes.byref(payload) if payload else None,
+            _ptr(d_payload_len), _ptr(d_status), _stream(stream)), "noise_gpu_hs_read_message")
+
+    def status(self, d_status, stream=None):
+        _check(self.lib.noise_gpu_hs_status(self.h, _ptr(d_status), _stream(stream)),
+               "noise_gpu_hs_status")
+
+    def split(self, d_k1, d_k2, d_hash=None, d_rs=None, stream=None):
+        _check(self.lib.noise_gpu_hs_split(self.h, _ptr(d_k1), _ptr(d_k2), _ptr(d_hash), _ptr(d_rs),
+                                           _stream(stream)), "noise_gpu_hs_split")
 
 
 # ---- host-buffer entry points (CipherState single-record path) ------------

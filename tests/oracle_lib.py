@@ -69,7 +69,21 @@ class Oracle:
                                             ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64,
                                             ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
             R.ref_batch_uniform.restype = ctypes.c_double
+            R.ref_xx_handshake.argtypes = [ctypes.c_char_p] * 4 + [ctypes.c_void_p] * 4
+            R.ref_xx_handshake.restype = ctypes.c_int
+            R.ref_xx_bench.argtypes = [ctypes.c_long, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+            R.ref_xx_bench.restype = ctypes.c_double
             self.ref = R
+
+    def ref_xx_handshake(self, si, ei, sr, er):
+        """Both parties of Noise_XX_25519_ChaChaPoly_BLAKE2b on the reference's
+        Monocypher primitives (oracle/ref_harness.c), empty prologue and
+        payloads: (msg1, msg2, msg3, handshake_hash, k1, k2)."""
+        msgs, h = ctypes.create_string_buffer(192), ctypes.create_string_buffer(64)
+        k1, k2 = ctypes.create_string_buffer(32), ctypes.create_string_buffer(32)
+        assert self.ref.ref_xx_handshake(si, ei, sr, er, msgs, h, k1, k2) == 0
+        m = msgs.raw
+        return m[:32], m[32:128], m[128:192], h.raw, k1.raw, k2.raw
 
     def encrypt(self, key, n, ad, pt, lib=None):
         lib = lib or self.lib

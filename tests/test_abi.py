@@ -76,3 +76,28 @@ def test_cipherstate_host_rules():
     r = subprocess.run([exe, "--host-only"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "PASSED" in r.stdout
+
+
+def test_handshake_batch_argument_validation():
+    """noise_gpu_hs_*: names and counts are checked before any device call;
+    NULL handles are refused; destroy(NULL) is a no-op."""
+    lib = noise_amd.load()
+    h = ctypes.c_void_p()
+    assert lib.noise_gpu_hs_create(b"XY", 1, 16, ctypes.byref(h)) == noise_amd.E_ARG
+    assert b"unknown handshake pattern" in lib.noise_gpu_last_error()
+    assert lib.noise_gpu_hs_create(b"XXpsk9", 1, 16, ctypes.byref(h)) == noise_amd.E_ARG
+    assert lib.noise_gpu_hs_create(b"XX", 1, 0, ctypes.byref(h)) == noise_amd.E_ARG
+    assert lib.noise_gpu_hs_create(None, 1, 16, ctypes.byref(h)) == noise_amd.E_ARG
+    assert lib.noise_gpu_hs_destroy(None) == noise_amd.OK
+    info = noise_amd.HsInfo()
+    assert lib.noise_gpu_hs_info_get(None, ctypes.byref(info)) == noise_amd.E_ARG
+    assert lib.noise_gpu_hs_start(None, None, None) == noise_amd.E_ARG
+    assert lib.noise_gpu_hs_split(None, None, None, None, None, None) == noise_amd.E_ARG
+    assert ctypes.sizeof(noise_amd.Span) == 40 and ctypes.sizeof(noise_amd.HsInfo) == 24
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a GPU is visible")
+def test_handshake_batch_needs_a_device():
+    h = ctypes.c_void_p()
+    assert noise_amd.load().noise_gpu_hs_create(b"XX", 1, 16, ctypes.byref(h)) == noise_amd.E_NODEV
+    assert not h.value

@@ -90,3 +90,72 @@ def test_handshake_vector_fixture_present():
     rows = [l.split("\t") for l in open(path).read().splitlines() if l]
     assert len(rows) == 110 and all(len(r) == 13 for r in rows)
     assert all(r[0].endswith("_25519_ChaChaPoly_BLAKE2b") for r in rows)
+
+
+def _py_xx(si, ei, sr, er):
+    """Noise_XX_25519_ChaChaPoly_BLAKE2b, both parties, empty prologue and
+    payloads, in plain Python (rev34 §5, hashlib BLAKE2b, the Python X25519
+    ladder and AEAD of tests/golden/make_fixtures.py): test infrastructure
+    pinning oracle/ref_harness.c:ref_xx_handshake."""
+    import make_fixtures as mf
+
+    def hkdf(ck, ikm):
+        tk = hmac.new(ck, ikm, hashlib.blake2b).digest()
+        o1 = hmac.new(tk, b"\x01", hashlib.blake2b).digest()
+        return o1, hmac.new(tk, o1 + b"\x02", hashlib.blake2b).digest()
+
+    class Sym:
+        def __init__(self):
+            self.h = b"Noise_XX_25519_ChaChaPoly_BLAKE2b".ljust(64, b"\0")
+            self.ck, self.k, self.n = self.h, None, 0
+            self.mix_hash(b"")
+
+        def mix_hash(self, d):
+            self.h = hashlib.blake2b(self.h + d).digest()
+
+        def mix_key(self, ikm):
+            self.ck, t = hkdf(self.ck, ikm)
+            self.k, self.n = t[:32], 0
+
+        def enc(self, pt):
+            ct = pt if self.k is None else mf.aead_encrypt(self.k, self.n, self.h, pt)
+            self.n += self.k is not None
+            self.mix_hash(ct)
+            return ct
+
+        def dec(self, ct):
+            pt = ct if self.k is None else mf.aead_decrypt(self.k, self.n, self.h, ct)
+            self.n += self.k is not None
+            self.mix_hash(ct)
+            return pt
+
+    pub = lambda sk: mf.x25519(sk, (9).to_bytes(32, "little"))  # noqa: E731
+    I, R = Sym(), Sym()
+    m1 = pub(ei)
+    I.mix_hash(m1); I.enc(b"")
+    R.mix_hash(m1); R.dec(b"")
+    epr = pub(er)
+    R.mix_hash(epr); R.mix_key(mf.x25519(er, m1))
+    m2 = epr + R.enc(pub(sr))
+    R.mix_key(mf.x25519(sr, m1)); m2 += R.enc(b"")
+    I.mix_hash(m2[:32]); I.mix_key(mf.x25519(ei, m2[:32]))
+    rs = I.dec(m2[32:80]); I.mix_key(mf.x25519(ei, rs)); I.dec(m2[80:])
+    m3 = I.enc(pub(si)); I.mix_key(mf.x25519(si, m2[:32])); m3 += I.enc(b"")
+    rsr = R.dec(m3[:48]); R.mix_key(mf.x25519(er, rsr)); R.dec(m3[48:])
+    assert I.h == R.h and rsr == pub(si) and rs == pub(sr)
+    k1, k2 = hkdf(I.ck, b"")
+    return m1, m2, m3, I.h, k1[:32], k2[:32]
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_reference_primitive_xx_matches_spec(oracle, seed):
+    """oracle/ref_harness.c:ref_xx_handshake (the reference's Monocypher
+    primitives composed as noise.cpp composes them, spec HasKey) equals an
+    independent Python XX: it is then the per-session checker of the batched
+    GPU handshake (tests/test_gpu_handshake_batch.py) and the CPU baseline of
+    tools/bench_handshake.py."""
+    if oracle.ref is None:
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    rng = random.Random(seed)
+    keys = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(4)]
+    assert oracle.ref_xx_handshake(*keys) == _py_xx(*keys)

@@ -587,30 +587,85 @@ static inline unsigned capped(uint64_t want, uint64_t cap) {
   return (unsigned)(want < cap ? want : cap);
 }
 
+// Fork/join companion of a caller stream: a non-blocking stream and two
+// events, cached per (device, stream) like the scratch.  The records DAG has
+// two independent branches after the classifier (below); the short ones run
+// on the companion stream while the segment kernel fills the GPU.
+struct AuxStream {
+  hipStream_t aux = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+static hipError_t aux_get(AuxStream *out, hipStream_t stream) {
+  struct Entry {
+    int dev;
+    hipStream_t stream;
+    AuxStream a;
+  };
+  static std::mutex mu;
+  static std::vector<Entry> cache;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lk(mu);
+  for (const Entry &en : cache)
+    if (en.dev == dev && en.stream == stream) {
+      *out = en.a;
+      return hipSuccess;
+    }
+  AuxStream a;
+  if ((e = hipStreamCreateWithFlags(&a.aux, hipStreamNonBlocking)) != hipSuccess) return e;
+  if ((e = hipEventCreateWithFlags(&a.fork, hipEventDisableTiming)) != hipSuccess) return e;
+  if ((e = hipEventCreateWithFlags(&a.join, hipEventDisableTiming)) != hipSuccess) return e;
+  cache.push_back({dev, stream, a});
+  *out = a;
+  return hipSuccess;
+}
+
+// After the classifier, two branches (both read only the classifier's output):
+//   caller stream : k_seg_prep -> segment tile kernel ------ join -> finalize
+//                                                                  (-> fixup)
+//   companion     : (fork after prep) tails, the five small tile classes,
+//                   the generic kernel ----------------------^
+// The segment kernel is the long pole (~80 % of a config-4 call); the
+// companion branch's launches are short or under-filled (the tails kernel has
+// one lane per tail) and now overlap it instead of following it.
 template <bool DECRYPT>
-static void launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr *hdr,
-                           const uint8_t *keys, const uint32_t *tails, uint64_t segbound,
-                           const uint8_t *in, uint8_t *out, uint8_t *status,
-                           hipStream_t stream) {
+static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr *hdr,
+                                 const uint8_t *keys, uint32_t nkeys,
+                                 const noise_gpu_record *recs, const uint32_t *idx,
+                                 const uint32_t *tails, uint64_t segbound, const uint8_t *in,
+                                 uint8_t *out, const uint8_t *ad, uint8_t *status,
+                                 hipStream_t stream) {
+  AuxStream ax;
+  hipError_t e = aux_get(&ax, stream);
+  if (e != hipSuccess) return e;
   const dim3 bt(64);
   const dim3 grid(capped((nrec + 63) / 64, NOISE_GRID_CAP));
+  SegRec *rt = const_cast<SegRec *>(ta.rt);
+  hipLaunchKernelGGL(k_seg_prep, grid, bt, 0, stream, keys, rt, hdr);
+  if ((e = hipEventRecord(ax.fork, stream)) != hipSuccess) return e;
+  if ((e = hipStreamWaitEvent(ax.aux, ax.fork, 0)) != hipSuccess) return e;
+  // companion branch
+  hipLaunchKernelGGL((k_seg_tail<DECRYPT>), grid, bt, 0, ax.aux, tails, rt, hdr, in, out);
   TileArgs a = ta;
 #define NOISE_DESC_TILE(C, LEN)                                                \
   a.cls = C;                                                                   \
-  hipLaunchKernelGGL((k_aead_tile<DECRYPT, LEN, false, kTileDesc>), grid, bt, 0, stream, a);
+  hipLaunchKernelGGL((k_aead_tile<DECRYPT, LEN, false, kTileDesc>), grid, bt, 0, ax.aux, a);
   NOISE_DESC_TILE(0, 64)
   NOISE_DESC_TILE(1, 128)
   NOISE_DESC_TILE(2, 192)
   NOISE_DESC_TILE(3, 256)
   NOISE_DESC_TILE(4, 512)
 #undef NOISE_DESC_TILE
-  // long records: prep -> every full segment in one tile launch + the tails
-  // -> finalize (-> decrypt: fix-up of records whose tag failed)
-  SegRec *rt = const_cast<SegRec *>(ta.rt);
-  hipLaunchKernelGGL(k_seg_prep, grid, bt, 0, stream, keys, rt, hdr);
+  const uint64_t gblocks = (nrec + kGenBlock - 1) / kGenBlock;
+  const dim3 gg((unsigned)(gblocks < 2 * NOISE_GRID_CAP ? gblocks : 2 * NOISE_GRID_CAP));
+  hipLaunchKernelGGL((k_aead_records<DECRYPT>), gg, dim3(kGenBlock), 0, ax.aux, keys, nkeys, recs,
+                     nrec, idx, hdr, in, out, ad, status);
+  if ((e = hipEventRecord(ax.join, ax.aux)) != hipSuccess) return e;
+  // caller-stream branch: every full segment of every long record
   const dim3 gseg(capped((segbound + 63) / 64, NOISE_GRID_CAP));
   hipLaunchKernelGGL((k_aead_tile<DECRYPT, 1024, false, kTileSeg>), gseg, bt, 0, stream, a);
-  hipLaunchKernelGGL((k_seg_tail<DECRYPT>), grid, bt, 0, stream, tails, rt, hdr, in, out);
+  if ((e = hipStreamWaitEvent(stream, ax.join, 0)) != hipSuccess) return e;
   hipLaunchKernelGGL((k_seg_finalize<DECRYPT>), grid, bt, 0, stream, ta.rt, ta.partial, hdr,
                      in, out, status);
   if (DECRYPT) {
@@ -618,6 +673,7 @@ static void launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr *hdr,
     hipLaunchKernelGGL(k_seg_fixup, gfix, bt, 0, stream, ta.segs, tails, ta.rt, hdr, in, out,
                        status);
   }
+  return hipGetLastError();
 }
 
 hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
@@ -685,15 +741,10 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   ta.rt = rt;
   ta.partial = partial;
   ta.nseg = &hdr->nseg;
-  if (decrypt) launch_classes<true>(ta, nrec, hdr, keys, tails, segcap, in, out, status, stream);
-  else launch_classes<false>(ta, nrec, hdr, keys, tails, segcap, in, out, status, stream);
-
-  const dim3 gg((unsigned)(gblocks < 2 * NOISE_GRID_CAP ? gblocks : 2 * NOISE_GRID_CAP));
-  if (decrypt)
-    hipLaunchKernelGGL((k_aead_records<true>), gg, bg, 0, stream, keys, nkeys, recs, nrec, idx, hdr, in, out, ad, status);
-  else
-    hipLaunchKernelGGL((k_aead_records<false>), gg, bg, 0, stream, keys, nkeys, recs, nrec, idx, hdr, in, out, ad, status);
-  return hipGetLastError();
+  return decrypt ? launch_classes<true>(ta, nrec, hdr, keys, nkeys, recs, idx, tails, segcap, in,
+                                       out, ad, status, stream)
+                 : launch_classes<false>(ta, nrec, hdr, keys, nkeys, recs, idx, tails, segcap, in,
+                                         out, ad, status, stream);
 }
 
 }  // namespace noise_amd

@@ -49,6 +49,9 @@ enum {
   hipErrorMemoryAllocation = 2,
 };
 typedef void *hipStream_t;
+typedef void *hipEvent_t;
+#define hipStreamNonBlocking 1u
+#define hipEventDisableTiming 2u
 
 namespace emu {
 
@@ -178,6 +181,19 @@ inline unsigned long long atomicMin(unsigned long long *p, unsigned long long v)
   emu::launch(kernel, dim3(grid), dim3(block), __VA_ARGS__)
 
 inline hipError_t hipGetLastError() { return hipSuccess; }
+// launches run synchronously in program order: streams and events are no-ops
+inline hipError_t hipStreamCreateWithFlags(hipStream_t *s, unsigned) {
+  static int tag;
+  *s = &tag;
+  return hipSuccess;
+}
+inline hipError_t hipEventCreateWithFlags(hipEvent_t *e, unsigned) {
+  static int tag;
+  *e = &tag;
+  return hipSuccess;
+}
+inline hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
+inline hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned) { return hipSuccess; }
 inline hipError_t hipGetDevice(int *d) { *d = 0; return hipSuccess; }
 inline hipError_t hipMalloc(void **p, size_t n) {
   *p = std::malloc(n);

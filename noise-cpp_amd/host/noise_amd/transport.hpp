@@ -13,7 +13,12 @@
 //     submission order.  Nonces are assigned at submit in each session's
 //     order, exactly as consecutive encrypt_with_ad / decrypt_with_ad calls
 //     would (decrypt advances n even when the tag fails, noise.cpp:421; the
-//     nonce limit 2^64-2 throws out_of_range, noise.cpp:398-400).
+//     nonce limit 2^64-2 throws out_of_range, noise.cpp:398-400);
+//   * Pipeline: the same batching over pinned ring slots for serving: a
+//     message is copied ONCE, from the caller's socket buffer into the
+//     pinned slot being filled; flush() launches that slot asynchronously
+//     (H2D, the records kernels, D2H on the slot's own stream) and filling
+//     continues in the next slot, so host copies, PCIe and the GPU overlap.
 #pragma once
 #include <cstddef>
 #include <cstdint>
@@ -76,6 +81,73 @@ class Batcher {
   Direction dir_;
   std::vector<Session> sessions_;
   std::vector<Item> queue_;
+};
+
+// Pinned, multi-slot, asynchronous form of Batcher (same nonce / length /
+// failure semantics).  Usage:
+//   Pipeline p(Pipeline::Direction::Encrypt);
+//   auto s = p.add_session(cs);
+//   while (more) { if (!p.submit(s, buf, n)) { tickets.push(p.flush()); p.submit(s, buf, n); } }
+//   auto b = p.wait(tickets.front());   // b.data(i) / b.length(i) / b.ok(i)
+// A Batch view stays valid until its slot is refilled, i.e. until `depth - 1`
+// further flushes; flush() blocks only when the slot it moves on to is still
+// in flight (back-pressure).  Session keys are uploaded to a device key table
+// once, when the session is added; not thread-safe (like CipherState).
+class Pipeline {
+ public:
+  using Direction = Batcher::Direction;
+  struct Options {
+    std::size_t slot_bytes = std::size_t(32) << 20;  // message bytes per slot
+    std::size_t slot_records = std::size_t(1) << 16; // messages per slot
+    int depth = 3;                                   // slots in the ring
+  };
+  class Batch {
+   public:
+    [[nodiscard]] std::size_t size() const { return n_; }
+    [[nodiscard]] std::size_t session(std::size_t i) const;
+    [[nodiscard]] std::uint64_t nonce(std::size_t i) const;
+    [[nodiscard]] bool ok(std::size_t i) const;                 // decrypt: tag verified
+    [[nodiscard]] const std::uint8_t *data(std::size_t i) const;  // ct || tag / plaintext
+    [[nodiscard]] std::size_t length(std::size_t i) const;
+
+   private:
+    friend class Pipeline;
+    const std::uint8_t *h_ = nullptr;
+    std::size_t n_ = 0, o_out_ = 0, o_st_ = 0;
+    bool dec_ = false;
+  };
+
+  explicit Pipeline(Direction d) : Pipeline(d, Options{}) {}
+  Pipeline(Direction d, const Options &o);
+  ~Pipeline();
+  Pipeline(const Pipeline &) = delete;
+  Pipeline &operator=(const Pipeline &) = delete;
+
+  std::size_t add_session(const CipherState &cs);
+  // copy one message into the filling slot and assign its nonce; false (and
+  // nothing consumed) when the slot has no room -- flush() and retry
+  bool submit(std::size_t s, const std::uint8_t *msg, std::size_t len);
+  [[nodiscard]] std::size_t pending() const;
+  // launch the filling slot; its ticket (0 if it was empty)
+  std::uint64_t flush();
+  // block until a flushed slot is done
+  Batch wait(std::uint64_t ticket);
+  [[nodiscard]] std::uint64_t nonce(std::size_t s) const { return nonces_.at(s); }
+  [[nodiscard]] CipherState state(std::size_t s) const;
+
+ private:
+  struct Slot;
+  void sync_all();
+  void grow_keys();
+  Direction dir_;
+  Options opt_;
+  std::size_t o_in_ = 0, o_out_ = 0, o_st_ = 0, slot_total_ = 0;
+  std::vector<Slot *> slots_;
+  std::size_t fill_ = 0;          // slot being filled
+  std::uint64_t tickets_ = 0;
+  std::vector<std::uint64_t> nonces_;
+  std::uint8_t *h_keys_ = nullptr, *d_keys_ = nullptr;  // pinned mirror / device table
+  std::size_t key_cap_ = 0, key_dirty_ = 0;
 };
 
 }  // namespace noise::transport

@@ -7,6 +7,8 @@
 #include <stdexcept>
 #include <string>
 
+#include <hip/hip_runtime_api.h>
+
 #include "noise_gpu.h"
 
 namespace noise::transport {
@@ -104,6 +106,218 @@ std::vector<Batcher::Result> Batcher::flush() {
   }
   queue_.clear();
   return out;
+}
+
+// ---- Pipeline ---------------------------------------------------------------
+namespace {
+void hip_check(hipError_t e, const char *what) {
+  if (e != hipSuccess)
+    throw std::runtime_error(std::string("noise-mi355x pipeline: ") + what + ": " + hipGetErrorString(e));
+}
+inline std::size_t align16(std::size_t x) { return (x + 15) & ~std::size_t(15); }
+inline std::size_t align256(std::size_t x) { return (x + 255) & ~std::size_t(255); }
+}  // namespace
+
+// One ring slot: pinned host image and device image of
+// [records | message bytes in | message bytes out | status]
+struct Pipeline::Slot {
+  std::uint8_t *h = nullptr, *d = nullptr;
+  hipStream_t st = nullptr;
+  hipEvent_t done = nullptr;
+  std::size_t nrec = 0, in_used = 0, out_used = 0;
+  std::uint64_t ticket = 0;
+  bool in_flight = false;
+  noise_gpu_record *recs() { return reinterpret_cast<noise_gpu_record *>(h); }
+};
+
+Pipeline::Pipeline(Direction d, const Options &o) : dir_(d), opt_(o) {
+  if (opt_.depth < 2 || opt_.slot_records == 0 || opt_.slot_bytes < 65536)
+    throw std::invalid_argument("pipeline: depth >= 2, slot_records >= 1, slot_bytes >= 64 KiB");
+  o_in_ = align256(opt_.slot_records * sizeof(noise_gpu_record));
+  o_out_ = align256(o_in_ + opt_.slot_bytes);
+  o_st_ = align256(o_out_ + opt_.slot_bytes + 16 * opt_.slot_records);
+  slot_total_ = o_st_ + opt_.slot_records;
+  for (int i = 0; i < opt_.depth; ++i) {
+    Slot *sl = new Slot();
+    slots_.push_back(sl);
+    hip_check(hipHostMalloc(reinterpret_cast<void **>(&sl->h), slot_total_, hipHostMallocDefault),
+              "pinned slot");
+    hip_check(hipMalloc(reinterpret_cast<void **>(&sl->d), slot_total_), "device slot");
+    hip_check(hipStreamCreateWithFlags(&sl->st, hipStreamNonBlocking), "slot stream");
+    hip_check(hipEventCreateWithFlags(&sl->done, hipEventDisableTiming), "slot event");
+  }
+}
+
+Pipeline::~Pipeline() {
+  try {
+    sync_all();
+  } catch (...) {
+  }
+  if (h_keys_) {
+    volatile std::uint8_t *kv = h_keys_;
+    for (std::size_t i = 0; i < 32 * key_cap_; ++i) kv[i] = 0;
+    (void)hipHostFree(h_keys_);
+  }
+  if (d_keys_) {
+    (void)hipMemset(d_keys_, 0, 32 * key_cap_);
+    (void)hipDeviceSynchronize();
+    (void)hipFree(d_keys_);
+  }
+  for (Slot *sl : slots_) {
+    if (sl->h) (void)hipHostFree(sl->h);
+    if (sl->d) (void)hipFree(sl->d);
+    if (sl->st) (void)hipStreamDestroy(sl->st);
+    if (sl->done) (void)hipEventDestroy(sl->done);
+    delete sl;
+  }
+}
+
+void Pipeline::sync_all() {
+  for (Slot *sl : slots_)
+    if (sl->in_flight) hip_check(hipEventSynchronize(sl->done), "slot wait");
+}
+
+void Pipeline::grow_keys() {
+  // the device table may be read by slots in flight: let them finish first
+  sync_all();
+  const std::size_t cap = key_cap_ ? 2 * key_cap_ : 1024;
+  std::uint8_t *h = nullptr, *d = nullptr;
+  hip_check(hipHostMalloc(reinterpret_cast<void **>(&h), 32 * cap, hipHostMallocDefault), "pinned keys");
+  hip_check(hipMalloc(reinterpret_cast<void **>(&d), 32 * cap), "device keys");
+  if (key_cap_) {
+    std::memcpy(h, h_keys_, 32 * key_cap_);
+    hip_check(hipMemcpy(d, d_keys_, 32 * key_cap_, hipMemcpyDeviceToDevice), "key table copy");
+    volatile std::uint8_t *kv = h_keys_;
+    for (std::size_t i = 0; i < 32 * key_cap_; ++i) kv[i] = 0;
+    (void)hipHostFree(h_keys_);
+    (void)hipMemset(d_keys_, 0, 32 * key_cap_);
+    (void)hipDeviceSynchronize();
+    (void)hipFree(d_keys_);
+  }
+  h_keys_ = h;
+  d_keys_ = d;
+  key_cap_ = cap;
+}
+
+std::size_t Pipeline::add_session(const CipherState &cs) {
+  const std::size_t s = nonces_.size();
+  if (s >= 0xffffffffu) throw std::length_error("pipeline: too many sessions");
+  if (s == key_cap_) grow_keys();
+  const std::array<std::uint8_t, 32> k = cs.key_material();
+  std::memcpy(h_keys_ + 32 * s, k.data(), 32);
+  nonces_.push_back(cs.nonce());
+  return s;
+}
+
+CipherState Pipeline::state(std::size_t s) const {
+  if (s >= nonces_.size()) throw std::out_of_range("pipeline: no such session");
+  std::array<std::uint8_t, 32> k;
+  std::memcpy(k.data(), h_keys_ + 32 * s, 32);
+  CipherState cs;
+  cs.initialize_key(k);
+  cs.set_nonce(nonces_[s]);
+  return cs;
+}
+
+std::size_t Pipeline::pending() const { return slots_[fill_]->nrec; }
+
+bool Pipeline::submit(std::size_t s, const std::uint8_t *msg, std::size_t len) {
+  std::uint64_t &n = nonces_.at(s);
+  const bool dec = dir_ == Direction::Decrypt;
+  if (n == std::numeric_limits<std::uint64_t>::max() - 1)  // noise.cpp:398-400
+    throw std::out_of_range("Nonce limit has been exceeded!");
+  if (!dec && len + 16 > kMaxMessage) throw std::length_error("Noise message exceeds 65535 bytes");
+  if (dec && (len < 16 || len > kMaxMessage)) throw std::invalid_argument("Invalid MAC");
+  Slot &sl = *slots_[fill_];
+  const std::size_t in_len = align16(len), out_len = dec ? align16(len - 16) : align16(len + 16);
+  if (sl.nrec == opt_.slot_records || sl.in_used + in_len > opt_.slot_bytes) return false;
+  if (len) std::memcpy(sl.h + o_in_ + sl.in_used, msg, len);
+  sl.recs()[sl.nrec] = noise_gpu_record{sl.in_used, sl.out_used, n, 0,
+                                        (std::uint32_t)(dec ? len - 16 : len), 0,
+                                        (std::uint32_t)s, 0};
+  sl.in_used += in_len;
+  sl.out_used += out_len;
+  ++sl.nrec;
+  ++n;  // decrypt: advances whatever the tag says (noise.cpp:421)
+  return true;
+}
+
+std::uint64_t Pipeline::flush() {
+  Slot &sl = *slots_[fill_];
+  if (sl.nrec == 0) return 0;
+  const bool dec = dir_ == Direction::Decrypt;
+  const std::size_t nkeys = nonces_.size();
+  if (key_dirty_ < nkeys) {  // new sessions' keys (rows never change once written)
+    hip_check(hipMemcpyAsync(d_keys_ + 32 * key_dirty_, h_keys_ + 32 * key_dirty_,
+                             32 * (nkeys - key_dirty_), hipMemcpyHostToDevice, sl.st), "key upload");
+    key_dirty_ = nkeys;
+  }
+  hip_check(hipMemcpyAsync(sl.d, sl.h, sl.nrec * sizeof(noise_gpu_record), hipMemcpyHostToDevice, sl.st),
+            "records H2D");
+  if (sl.in_used)
+    hip_check(hipMemcpyAsync(sl.d + o_in_, sl.h + o_in_, sl.in_used, hipMemcpyHostToDevice, sl.st),
+              "messages H2D");
+  const auto *d_recs = reinterpret_cast<const noise_gpu_record *>(sl.d);
+  const int rc = dec ? noise_gpu_decrypt_records(d_keys_, (std::uint32_t)nkeys, d_recs, sl.nrec, sl.d + o_in_,
+                                                 sl.d + o_out_, nullptr, sl.d + o_st_, sl.st)
+                     : noise_gpu_encrypt_records(d_keys_, (std::uint32_t)nkeys, d_recs, sl.nrec, sl.d + o_in_,
+                                                 sl.d + o_out_, nullptr, sl.st);
+  if (rc != NOISE_GPU_OK)
+    throw std::runtime_error(std::string("noise-mi355x: ") + noise_gpu_strerror(rc) + ": " +
+                             noise_gpu_last_error());
+  if (sl.out_used)
+    hip_check(hipMemcpyAsync(sl.h + o_out_, sl.d + o_out_, sl.out_used, hipMemcpyDeviceToHost, sl.st),
+              "messages D2H");
+  if (dec)
+    hip_check(hipMemcpyAsync(sl.h + o_st_, sl.d + o_st_, sl.nrec, hipMemcpyDeviceToHost, sl.st),
+              "status D2H");
+  hip_check(hipEventRecord(sl.done, sl.st), "slot event");
+  sl.in_flight = true;
+  sl.ticket = ++tickets_;
+  // move on; a slot still in flight is waited for here (back-pressure), and
+  // its results are gone once refilled
+  fill_ = (fill_ + 1) % slots_.size();
+  Slot &nx = *slots_[fill_];
+  if (nx.in_flight) {
+    hip_check(hipEventSynchronize(nx.done), "slot wait");
+    nx.in_flight = false;
+  }
+  nx.nrec = nx.in_used = nx.out_used = 0;
+  nx.ticket = 0;
+  return sl.ticket;
+}
+
+Pipeline::Batch Pipeline::wait(std::uint64_t ticket) {
+  Slot *sl = nullptr;
+  for (Slot *c : slots_)
+    if (c->ticket == ticket && ticket != 0) sl = c;
+  if (!sl) throw std::logic_error("pipeline: ticket unknown or its slot was reused");
+  if (sl->in_flight) {
+    hip_check(hipEventSynchronize(sl->done), "slot wait");
+    sl->in_flight = false;
+  }
+  Batch b;
+  b.h_ = sl->h;
+  b.n_ = sl->nrec;
+  b.o_out_ = o_out_;
+  b.o_st_ = o_st_;
+  b.dec_ = dir_ == Direction::Decrypt;
+  return b;
+}
+
+std::size_t Pipeline::Batch::session(std::size_t i) const {
+  return reinterpret_cast<const noise_gpu_record *>(h_)[i].key_idx;
+}
+std::uint64_t Pipeline::Batch::nonce(std::size_t i) const {
+  return reinterpret_cast<const noise_gpu_record *>(h_)[i].nonce;
+}
+bool Pipeline::Batch::ok(std::size_t i) const { return !dec_ || h_[o_st_ + i] == NOISE_GPU_REC_OK; }
+const std::uint8_t *Pipeline::Batch::data(std::size_t i) const {
+  return h_ + o_out_ + reinterpret_cast<const noise_gpu_record *>(h_)[i].out_off;
+}
+std::size_t Pipeline::Batch::length(std::size_t i) const {
+  const std::size_t len = reinterpret_cast<const noise_gpu_record *>(h_)[i].len;
+  return dec_ ? len : len + 16;
 }
 
 }  // namespace noise::transport

@@ -2,15 +2,26 @@
 // against the CPU oracle (oracle/liboracle.so: test infrastructure).
 //
 //   transport_test <sessions> <messages> <seed>
+//   transport_test pipeline <sessions> <messages> <seed>  the same through
+//       noise::transport::Pipeline (small slots: many flushes in flight,
+//       full-slot retries, ticket reuse), ciphertexts vs the oracle and vs
+//       the Batcher's, decrypt round trip with tampered records
+//   transport_test bench <batcher|pipeline> <sessions> <messages> <len>
+//       host-resident throughput, encrypt then decrypt, GiB/s of plaintext
 // Sessions get random keys and start nonces; messages (0..2000 bytes, some
 // 65519) are submitted interleaved, encrypted in ONE batch, checked bit-exact
 // against oracle_noise_encrypt with each session's nonce sequence, framed per
 // session into a byte stream, re-read through a Deframer fed in random-size
 // chunks, decrypted in ONE batch (one record tampered per 97) and compared.
+#include <hip/hip_runtime_api.h>
+
+#include <chrono>
 #include <cstdio>
+#include <deque>
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <string>
 #include <vector>
 
 #include "noise_amd/transport.hpp"
@@ -23,7 +34,213 @@ void oracle_noise_encrypt(const uint8_t key[32], uint64_t n, const uint8_t *ad, 
 using bytes = std::vector<std::uint8_t>;
 namespace nt = noise::transport;
 
+static int run_pipeline(int S, int M, std::uint64_t seed) {
+  std::mt19937_64 rng(seed);
+  int fails = 0;
+  auto check = [&](bool c, const char *what, long i) {
+    if (!c && fails++ < 20) std::printf("FAIL %s (%ld)\n", what, i);
+  };
+  nt::Pipeline::Options o;
+  o.slot_bytes = 256 << 10;  // small slots: many flushes, full-slot retries
+  o.slot_records = 97;
+  o.depth = 3;
+  nt::Pipeline enc(nt::Pipeline::Direction::Encrypt, o), dec(nt::Pipeline::Direction::Decrypt, o);
+  nt::Batcher ref(nt::Batcher::Direction::Encrypt);
+  std::vector<std::array<std::uint8_t, 32>> keys(S);
+  std::vector<std::uint64_t> n0(S);
+  for (int s = 0; s < S; ++s) {
+    for (auto &b : keys[s]) b = (std::uint8_t)rng();
+    n0[s] = rng() % 3 == 0 ? (1ull << 32) - 2 + (rng() % 5) : rng() % 1000;
+    noise::CipherState cs;
+    cs.initialize_key(keys[s]);
+    cs.set_nonce(n0[s]);
+    check(enc.add_session(cs) == (std::size_t)s && dec.add_session(cs) == (std::size_t)s &&
+              ref.add_session(cs) == (std::size_t)s, "session id", s);
+  }
+  std::vector<int> sess(M);
+  std::vector<bytes> pt(M), ct(M);
+  for (int i = 0; i < M; ++i) {
+    sess[i] = (int)(rng() % S);
+    const std::size_t len = rng() % 41 == 0 ? 65519 : rng() % 3 == 0 ? 1024 : rng() % 2001;
+    pt[i].resize(len);
+    for (auto &b : pt[i]) b = (std::uint8_t)rng();
+    ref.submit(sess[i], pt[i]);
+  }
+  // encrypt through the ring: a flush refills the slot of the ticket two
+  // flushes back, so at most depth - 2 tickets may stay unconsumed across it
+  std::deque<std::pair<std::uint64_t, int>> outstanding;  // ticket, first message index
+  int next_i = 0, done = 0, flushes = 0;
+  auto drain = [&](std::size_t keep) {
+    while (outstanding.size() > keep) {
+      auto [t, first] = outstanding.front();
+      outstanding.pop_front();
+      const nt::Pipeline::Batch b = enc.wait(t);
+      for (std::size_t j = 0; j < b.size(); ++j) {
+        const int i = first + (int)j;
+        check(b.session(j) == (std::size_t)sess[i] && b.ok(j) && b.length(j) == pt[i].size() + 16,
+              "pipeline result header", i);
+        ct[i].assign(b.data(j), b.data(j) + b.length(j));
+        ++done;
+      }
+    }
+  };
+  int first = 0;
+  while (next_i < M) {
+    if (enc.submit(sess[next_i], pt[next_i].data(), pt[next_i].size())) {
+      ++next_i;
+      continue;
+    }
+    outstanding.push_back({enc.flush(), first});
+    ++flushes;
+    first = next_i;
+    drain(o.depth - 2);  // the next flush reuses the slot of ticket t-2
+  }
+  if (enc.pending()) {
+    outstanding.push_back({enc.flush(), first});
+    ++flushes;
+  }
+  drain(0);
+  check(done == M, "all results", done);
+  bool threw = false;
+  try {
+    (void)enc.wait(1);  // long since reused
+  } catch (const std::logic_error &) {
+    threw = true;
+  }
+  check(threw || flushes <= o.depth, "stale ticket refused", flushes);
+  const std::vector<nt::Batcher::Result> want = ref.flush();
+  std::vector<std::uint64_t> next(n0);
+  bytes w(65535 + 16);
+  for (int i = 0; i < M; ++i) {
+    oracle_noise_encrypt(keys[sess[i]].data(), next[sess[i]]++, nullptr, 0, pt[i].data(), pt[i].size(),
+                         w.data());
+    check(ct[i].size() == pt[i].size() + 16 && std::memcmp(ct[i].data(), w.data(), ct[i].size()) == 0,
+          "pipeline ciphertext vs oracle", i);
+    check(ct[i] == want[i].msg, "pipeline vs batcher", i);
+  }
+  for (int s = 0; s < S; ++s) check(enc.nonce(s) == next[s], "encrypt nonce advance", s);
+  // decrypt, tampering every 89th; one flush at a time
+  std::vector<bytes> back(M);
+  std::vector<bool> okv(M);
+  int i0 = 0;
+  for (int i = 0; i <= M; ++i) {
+    bytes m;
+    if (i < M) {
+      m = ct[i];
+      if (i % 89 == 3) m[rng() % m.size()] ^= 0x10;
+      if (dec.submit(sess[i], m.data(), m.size())) continue;
+    }
+    const std::uint64_t t = dec.flush();
+    if (t) {
+      const nt::Pipeline::Batch b = dec.wait(t);
+      for (std::size_t j = 0; j < b.size(); ++j) {
+        okv[i0 + j] = b.ok(j);
+        if (b.ok(j)) back[i0 + j].assign(b.data(j), b.data(j) + b.length(j));
+      }
+      i0 += (int)b.size();
+    }
+    if (i < M) check(dec.submit(sess[i], m.data(), m.size()), "submit after flush", i);
+  }
+  check(i0 == M, "decrypt count", i0);
+  for (int i = 0; i < M; ++i) {
+    if (i % 89 == 3) check(!okv[i], "tampered rejected", i);
+    else check(okv[i] && back[i] == pt[i], "decrypt round trip", i);
+  }
+  for (int s = 0; s < S; ++s) check(dec.nonce(s) == next[s], "decrypt nonce advance", s);
+  std::printf("pipeline sessions %d messages %d flushes %d: %s (%d failures)\n", S, M, flushes,
+              fails ? "FAIL" : "ok", fails);
+  return fails ? 1 : 0;
+}
+
+// Host-resident throughput: M messages of len bytes from one source buffer
+// (the "socket reads"), encrypt then decrypt, results checksummed (touched).
+static int run_bench(const std::string &mode, int S, long M, std::size_t len) {
+  std::mt19937_64 rng(7);
+  bytes src((std::size_t)M * len);
+  for (std::size_t i = 0; i < src.size(); i += 8) {
+    const std::uint64_t v = rng();
+    std::memcpy(src.data() + i, &v, std::min<std::size_t>(8, src.size() - i));
+  }
+  std::vector<noise::CipherState> cs(S);
+  for (int s = 0; s < S; ++s) {
+    std::array<std::uint8_t, 32> k;
+    for (auto &b : k) b = (std::uint8_t)rng();
+    cs[s].initialize_key(k);
+  }
+  using clk = std::chrono::steady_clock;
+  std::uint64_t sum = 0;
+  double secs[2] = {0, 0};
+  bytes ctall((std::size_t)M * (len + 16));
+  // long-lived objects, as in a server: built (pinned slots, key upload)
+  // outside the timed region
+  nt::Pipeline penc(nt::Pipeline::Direction::Encrypt), pdec(nt::Pipeline::Direction::Decrypt);
+  for (int s = 0; s < S; ++s) {
+    penc.add_session(cs[s]);
+    pdec.add_session(cs[s]);
+  }
+  for (int pass = 0; pass < 3; ++pass) {  // pass 0 warms up (kernels, scratch)
+    for (int d = 0; d < 2; ++d) {
+      const bool dec = d == 1;
+      const std::size_t ilen = dec ? len + 16 : len;
+      const std::uint8_t *in = dec ? ctall.data() : src.data();
+      const auto t0 = clk::now();
+      if (mode == "batcher") {
+        nt::Batcher b(dec ? nt::Batcher::Direction::Decrypt : nt::Batcher::Direction::Encrypt);
+        for (int s = 0; s < S; ++s) b.add_session(cs[s]);
+        const long per = 1 << 16;
+        for (long i0 = 0; i0 < M; i0 += per) {
+          for (long i = i0; i < std::min(M, i0 + per); ++i)
+            b.submit(i % S, bytes(in + i * ilen, in + (i + 1) * ilen));
+          const auto r = b.flush();
+          for (std::size_t j = 0; j < r.size(); ++j) {
+            if (!dec) std::memcpy(ctall.data() + (i0 + j) * (len + 16), r[j].msg.data(), len + 16);
+            sum += r[j].msg[0];
+          }
+        }
+      } else {
+        nt::Pipeline &p = dec ? pdec : penc;
+        std::deque<std::pair<std::uint64_t, long>> q;
+        long first = 0;
+        auto take = [&](std::size_t keep) {
+          while (q.size() > keep) {
+            auto [t, f] = q.front();
+            q.pop_front();
+            const nt::Pipeline::Batch b = p.wait(t);
+            for (std::size_t j = 0; j < b.size(); ++j) {
+              if (!dec) std::memcpy(ctall.data() + (f + j) * (len + 16), b.data(j), len + 16);
+              else if (!b.ok(j)) throw std::runtime_error("bench: decrypt failed");
+              sum += b.data(j)[0];
+            }
+          }
+        };
+        for (long i = 0; i < M;) {
+          if (p.submit(i % S, in + i * ilen, ilen)) {
+            ++i;
+            continue;
+          }
+          q.push_back({p.flush(), first});
+          first = i;
+          take(1);  // depth 3: the next flush reuses the slot two back
+        }
+        q.push_back({p.flush(), first});
+        take(0);
+      }
+      const double t = std::chrono::duration<double>(clk::now() - t0).count();
+      if (pass > 0) secs[d] += t;
+    }
+  }
+  const double gib = (double)M * len * 2 / (1u << 30);  // two timed passes per direction
+  std::printf("{\"mode\": \"%s\", \"sessions\": %d, \"messages\": %ld, \"len\": %zu, "
+              "\"encrypt_gib_s\": %.2f, \"decrypt_gib_s\": %.2f, \"checksum\": %llu}\n",
+              mode.c_str(), S, M, len, gib / secs[0], gib / secs[1], (unsigned long long)sum);
+  return 0;
+}
+
 int main(int argc, char **argv) {
+  if (argc > 1 && std::string(argv[1]) == "pipeline")
+    return run_pipeline(std::atoi(argv[2]), std::atoi(argv[3]), std::strtoull(argv[4], nullptr, 0));
+  if (argc > 1 && std::string(argv[1]) == "bench")
+    return run_bench(argv[2], std::atoi(argv[3]), std::atol(argv[4]), std::strtoul(argv[5], nullptr, 0));
   const int S = argc > 1 ? std::atoi(argv[1]) : 100;
   const int M = argc > 2 ? std::atoi(argv[2]) : 1000;
   std::mt19937_64 rng(argc > 3 ? std::strtoull(argv[3], nullptr, 0) : 1);

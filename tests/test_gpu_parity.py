@@ -396,6 +396,19 @@ def test_transport_batcher(sessions, messages, seed):
     assert "ok (0 failures)" in r.stdout
 
 
+@pytest.mark.parametrize("sessions,messages,seed", [(50, 1500, 3), (400, 6000, 4)])
+def test_transport_pipeline(sessions, messages, seed):
+    """noise::transport::Pipeline (pinned ring slots, asynchronous flushes):
+    tiny slots force many flushes in flight and full-slot retries; ciphertexts
+    vs the CPU oracle and vs the Batcher, decrypt round trip with tampered
+    records, per-session nonce accounting, stale tickets refused."""
+    exe = os.path.join(noise_amd.ROOT, "noise-cpp_amd", "bin", "transport_test")
+    r = subprocess.run([exe, "pipeline", str(sessions), str(messages), str(seed)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "ok (0 failures)" in r.stdout
+
+
 def _sessions_case(rng, nkeys, per, length):
     keys = [rng.randbytes(32) for _ in range(nkeys)]
     nrec = nkeys * per

@@ -8,7 +8,8 @@ batches; the gap puts records past 2^31 bytes into their buffers (64-bit
 offsets whose low word has bit 31 set); "ragged" lengths 1..70000 give odd
 segment tails and > 65535-byte records (generic class); a 300-segment
 scratch cap forces the segment-overflow path.  Test infrastructure only: the
-product runs these kernels on the GPU (tests/test_gpu_records_mixed.py)."""
+product runs these kernels on the GPU (tests/test_gpu_records_mixed.py).
+The batched-handshake kernels run the same way (emu_handshake)."""
 import os
 import subprocess
 
@@ -60,3 +61,19 @@ def test_records_segment_overflow_emulated(emu_bin_small_cap):
     r = _run(emu_bin_small_cap, "cfg4", 700, 7, 0)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]
     assert "ok (0 failures)" in r.stdout
+
+
+def test_emulated_batched_handshakes():
+    """The batched-handshake kernels (csrc/handshake_kernels.hip) and their
+    host driver (csrc/handshake_batch.hip), unmodified, on the CPU under ASan:
+    the reference's 110 vectors through noise_gpu_hs_* -- messages, handshake
+    hashes, split keys, transport records under them vs the oracle."""
+    r = subprocess.run(["make", "-C", EMU, "handshake"], capture_output=True, text=True, timeout=900)
+    if r.returncode != 0:
+        pytest.fail("emulation build failed:\n" + r.stdout[-2000:] + r.stderr[-4000:])
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
+    r = subprocess.run([os.path.join(EMU, "build", "emu_handshake"),
+                        os.path.join(ROOT, "tests", "golden", "handshake_vectors.tsv")],
+                       capture_output=True, text=True, timeout=900, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "vectors 110, failed 0" in r.stdout and "transport records 211" in r.stdout, r.stdout

@@ -199,7 +199,26 @@ inline hipError_t hipMalloc(void **p, size_t n) {
   *p = std::malloc(n);
   return *p ? hipSuccess : hipErrorMemoryAllocation;
 }
+template <class T>
+inline hipError_t hipMalloc(T **p, size_t n) {  // HIP's typed overload
+  return hipMalloc(reinterpret_cast<void **>(p), n);
+}
 inline hipError_t hipFree(void *p) { std::free(p); return hipSuccess; }
+enum hipMemcpyKind { hipMemcpyHostToDevice, hipMemcpyDeviceToHost, hipMemcpyDeviceToDevice };
+inline hipError_t hipMemset(void *p, int v, size_t n) {
+  std::memset(p, v, n);
+  return hipSuccess;
+}
+inline hipError_t hipMemcpy(void *d, const void *s, size_t n, hipMemcpyKind) {
+  std::memmove(d, s, n);
+  return hipSuccess;
+}
+inline hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, hipMemcpyKind, hipStream_t) {
+  std::memmove(d, s, n);
+  return hipSuccess;
+}
+inline hipError_t hipDeviceSynchronize() { return hipSuccess; }
+inline const char *hipGetErrorString(hipError_t) { return "emulated HIP error"; }
 inline hipError_t hipMemsetAsync(void *p, int v, size_t n, hipStream_t) {
   std::memset(p, v, n);
   return hipSuccess;

@@ -130,9 +130,9 @@ __global__ __launch_bounds__(64) void k_hs_set_key(HsSession *S, uint64_t n, int
     for (int j = 0; j < 8; ++j) k[j] = blk[j];
   }
   store_key(row, which, k);
-  if (derive_pk) {
-    uint32_t u[8] = {9, 0, 0, 0, 0, 0, 0, 0}, pk[8];
-    x25519::scalarmult(pk, k, u);
+  if (derive_pk) {  // fixed-base public key (edwards25519 table, x25519_device.hpp)
+    uint32_t pk[8];
+    x25519::base_scalarmult(pk, k);
     store_key(row, which + 1, pk);
   }
 }

@@ -276,5 +276,132 @@ __device__ __forceinline__ void scalarmult(uint32_t out[8], const uint32_t kin[8
   fe_tobytes(out, x2);
 }
 
+// ---- fixed base: public keys X25519(k, 9) --------------------------------
+// [k]B on edwards25519 (the birational image of u = 9), then u = (Z+Y)/(Z-Y)
+// (RFC 7748 §4.1).  k is recoded into 64 signed radix-16 digits
+// d_i = n_i + b_(4i-1) - 16 b_(4i+3) in [-8, 8] (Booth: each digit from five
+// scalar bits, no carry chain), and [k]B = sum_i d_i 16^i B: 64 mixed
+// additions of table points kBaseTable[i][|d_i|-1] = |d_i| 16^i B (affine
+// niels form (y+x, y-x, 2dxy), tools/gen_base_table.py).  Constant time per
+// lane: every window reads all 8 entries of its row (the row index i is
+// public and wave-uniform, so they are scalar loads) and keeps the wanted one
+// with masks; a negative digit swaps y+x / y-x and negates 2dxy with masks.
+// ~2.9x fewer VALU instructions than the ladder with u = 9.
+static __constant__ const uint32_t kBaseTable[64][8][3][10] = {
+#include "ed25519_base_table.inc"
+};
+
+struct Niels {
+  Fe yp, ym, xy2d;
+};
+struct P3 {
+  Fe X, Y, Z, T;
+};
+
+__device__ __forceinline__ void fe_zero(Fe &h) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) h.v[i] = 0u;
+}
+__device__ __forceinline__ void fe_one(Fe &h) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) h.v[i] = i == 0 ? 1u : 0u;
+}
+__device__ __forceinline__ void fe_cmov(Fe &t, const Fe &e, uint32_t mask) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) t.v[i] ^= mask & (t.v[i] ^ e.v[i]);
+}
+
+// t = d * 16^i * B in niels form, d in [-8, 8] (secret), row i public
+__device__ __forceinline__ void base_select(Niels &t, int i, int32_t d) {
+  const uint32_t neg = (uint32_t)d >> 31;
+  const uint32_t mag = (uint32_t)((d ^ -(int32_t)neg) + (int32_t)neg);  // |d|
+  fe_one(t.yp);
+  fe_one(t.ym);
+  fe_zero(t.xy2d);
+#pragma unroll 1
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t m = 0u - (uint32_t)(mag == (uint32_t)(j + 1));
+    const uint32_t *e = kBaseTable[i][j][0];
+#pragma unroll
+    for (int l = 0; l < 10; ++l) {
+      t.yp.v[l] ^= m & (t.yp.v[l] ^ e[l]);
+      t.ym.v[l] ^= m & (t.ym.v[l] ^ e[10 + l]);
+      t.xy2d.v[l] ^= m & (t.xy2d.v[l] ^ e[20 + l]);
+    }
+  }
+  // -(x, y) = (-x, y): swap y+x and y-x, negate 2dxy
+  const uint32_t nm = 0u - neg;
+  Fe sw = t.yp, mx, z;
+  fe_cmov(t.yp, t.ym, nm);
+  fe_cmov(t.ym, sw, nm);
+  fe_zero(z);
+  fe_sub(mx, z, t.xy2d);  // 2p - 2dxy
+  fe_cmov(t.xy2d, mx, nm);
+}
+
+// h <- h + q (extended + affine niels: 7 multiplications).  Inputs carried;
+// every difference below has a carried subtrahend, every product input
+// stays < 2^27.7 per limb (fe_mul's bound).
+__device__ __forceinline__ void ge_madd(P3 &h, const Niels &q) {
+  Fe a, b, A, Bm, C, D, X1, Y1, Z1, T1;
+  fe_add(a, h.Y, h.X);
+  fe_sub(b, h.Y, h.X);
+  fe_mul(A, a, q.yp);
+  fe_mul(Bm, b, q.ym);
+  fe_mul(C, q.xy2d, h.T);
+  fe_add(D, h.Z, h.Z);
+  fe_reduce(D);
+  fe_sub(X1, A, Bm);
+  fe_add(Y1, A, Bm);
+  fe_add(Z1, D, C);
+  fe_sub(T1, D, C);
+  fe_mul(h.X, X1, T1);
+  fe_mul(h.Y, Y1, Z1);
+  fe_mul(h.Z, Z1, T1);
+  fe_mul(h.T, X1, Y1);
+}
+
+__device__ __forceinline__ void base_scalarmult(uint32_t out[8], const uint32_t kin[8]) {
+  uint32_t k[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) k[j] = kin[j];
+  k[0] &= ~7u;                                   // clamp (RFC 7748 §5)
+  k[7] = (k[7] & 0x7fffffffu) | 0x40000000u;
+  P3 h;  // identity (0 : 1 : 1 : 0)
+  fe_zero(h.X);
+  fe_one(h.Y);
+  fe_one(h.Z);
+  fe_zero(h.T);
+  uint32_t carry = 0;  // b_(4i-1)
+#pragma unroll 1
+  for (int i = 0; i < 64; ++i) {
+    uint32_t w;
+    switch (i >> 3) {  // wave-uniform
+      case 0: w = k[0]; break;
+      case 1: w = k[1]; break;
+      case 2: w = k[2]; break;
+      case 3: w = k[3]; break;
+      case 4: w = k[4]; break;
+      case 5: w = k[5]; break;
+      case 6: w = k[6]; break;
+      default: w = k[7]; break;
+    }
+    const uint32_t nib = (w >> (4 * (i & 7))) & 15u;
+    const uint32_t top = nib >> 3;
+    const int32_t d = (int32_t)(nib + carry) - (int32_t)(top << 4);
+    carry = top;
+    Niels t;
+    base_select(t, i, d);
+    ge_madd(h, t);
+  }
+  // bit 255 is clear after clamping: no final carry.  u = (Z + Y) / (Z - Y)
+  Fe num, den, u;
+  fe_add(num, h.Z, h.Y);
+  fe_sub(den, h.Z, h.Y);
+  fe_invert(den, den);
+  fe_mul(u, num, den);
+  fe_tobytes(out, u);
+}
+
 }  // namespace x25519
 }  // namespace noise_amd

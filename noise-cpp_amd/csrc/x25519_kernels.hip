@@ -3,7 +3,8 @@
 // reference's noise::dh -> crypto_x25519 (noise.cpp:172-177,
 // monocypher.c:1546-1563); written from RFC 7748 §5 (clamped scalar,
 // Montgomery ladder, a24 = 121665).  One lane = one scalar multiplication
-// (x25519_device.hpp).
+// (x25519_device.hpp); public keys (points == NULL) take the fixed-base
+// edwards25519 table path instead of the ladder.
 #include "x25519_device.hpp"
 #include "launchers.hpp"
 
@@ -15,20 +16,19 @@ __global__ __launch_bounds__(64) void k_x25519(const u32x4 *__restrict__ scalars
                                                u32x4 *__restrict__ out, uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * 64 + threadIdx.x;
   if (i >= n) return;
-  uint32_t k[8], u[8];
+  uint32_t k[8], w[8];
   {
     const u32x4 a = scalars[2 * i], b = scalars[2 * i + 1];
     k[0] = a.x; k[1] = a.y; k[2] = a.z; k[3] = a.w; k[4] = b.x; k[5] = b.y; k[6] = b.z; k[7] = b.w;
   }
   if (points) {
+    uint32_t u[8];
     const u32x4 a = points[2 * i], b = points[2 * i + 1];
     u[0] = a.x; u[1] = a.y; u[2] = a.z; u[3] = a.w; u[4] = b.x; u[5] = b.y; u[6] = b.z; u[7] = b.w;
-  } else {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) u[j] = j == 0 ? 9u : 0u;
+    x25519::scalarmult(w, k, u);
+  } else {  // public keys: the fixed-base table path (wave-uniform branch)
+    x25519::base_scalarmult(w, k);
   }
-  uint32_t w[8];
-  x25519::scalarmult(w, k, u);
   out[2 * i] = u32x4{w[0], w[1], w[2], w[3]};
   out[2 * i + 1] = u32x4{w[4], w[5], w[6], w[7]};
 }

@@ -77,3 +77,32 @@ def test_emulated_batched_handshakes():
                        capture_output=True, text=True, timeout=900, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "vectors 110, failed 0" in r.stdout and "transport records 211" in r.stdout, r.stdout
+
+
+def test_emulated_fixed_base_public_keys():
+    """x25519_device.hpp's fixed-base path (edwards25519 radix-16 table,
+    constant-time selects) on the CPU under ASan: RFC 7748 §6.1 and random /
+    extreme scalars against the device ladder with u = 9 and the host X25519."""
+    r = subprocess.run(["make", "-C", EMU, "handshake"], capture_output=True, text=True, timeout=900)
+    if r.returncode != 0:
+        pytest.fail("emulation build failed:\n" + r.stdout[-2000:] + r.stderr[-4000:])
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
+    r = subprocess.run([os.path.join(EMU, "build", "emu_x25519"), "300", "11"], capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "0 failures: ok" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def test_base_table_generator_is_current():
+    """noise-cpp_amd/csrc/ed25519_base_table.inc is what tools/gen_base_table.py
+    (exact big-integer edwards25519 arithmetic, self-checked) generates."""
+    import importlib.util
+    import tempfile
+    spec = importlib.util.spec_from_file_location("gen_base_table",
+                                                  os.path.join(ROOT, "tools", "gen_base_table.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    with tempfile.TemporaryDirectory() as d:
+        mod.OUT = os.path.join(d, "t.inc")
+        mod.main()
+        fresh = open(mod.OUT).read()
+    assert fresh == open(os.path.join(ROOT, "noise-cpp_amd", "csrc", "ed25519_base_table.inc")).read()

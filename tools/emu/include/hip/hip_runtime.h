@@ -26,6 +26,7 @@
 #define __forceinline__ inline
 #define __launch_bounds__(...)
 #define __shared__ static
+#define __constant__
 #define address_space(x) unused  // LDS pointers are plain pointers here
 
 struct uint4 {

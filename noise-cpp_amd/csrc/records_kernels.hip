@@ -43,7 +43,9 @@ constexpr int kClsGeneric = kNumTileCls + 1;
 constexpr int kNumCls = kNumTileCls + 2;
 constexpr int kColSegs = kNumCls;         // classifier column: full segments
 constexpr int kColTails = kNumCls + 1;    // classifier column: long records with a tail
-constexpr int kCols = kNumCls + 2;
+constexpr int kColFin0 = kNumCls + 2;     // classifier columns: long records by
+constexpr int kFinBuckets = 6;            // floor(log2(full segments)), 1..63 -> 0..5
+constexpr int kCols = kNumCls + 2 + kFinBuckets;
 #ifndef NOISE_CLASSIFY_MIN  // overridable for the CPU emulation build
 #define NOISE_CLASSIFY_MIN 2048
 #endif
@@ -87,9 +89,15 @@ struct RecHdr {
   unsigned long long cls_base[kCols];  // start of each class in idx
   unsigned long long nlong;            // long records handled as segments
   unsigned long long nseg;             // their full segments
-  unsigned long long pad[30 - 2 * kCols];
+  unsigned long long pad[62 - 2 * kCols];
 };
-static_assert(sizeof(RecHdr) == 256, "scratch header layout");
+static_assert(sizeof(RecHdr) == 512, "scratch header layout");
+
+// finalize-order bucket of a long record with nf >= 1 full segments
+__device__ __forceinline__ int fin_bucket(uint32_t nf) {
+  const int b = 31 - __builtin_clz(nf | 1u);
+  return b < kFinBuckets - 1 ? b : kFinBuckets - 1;
+}
 
 // wave-wide inclusive prefix sum (all 64 lanes participate)
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
@@ -118,7 +126,7 @@ __global__ __launch_bounds__(64) void k_cls_count(
   const uint32_t lane = threadIdx.x;
   const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
   const uint64_t e0 = b0 + chunk < nrec ? b0 + chunk : nrec;
-  uint32_t cnt[kNumCls] = {0}, nseg = 0, ntail = 0;
+  uint32_t cnt[kNumCls] = {0}, fin[kFinBuckets] = {0}, nseg = 0, ntail = 0;
 #pragma unroll 1
   for (uint64_t i0 = b0; i0 < e0; i0 += 64) {
     const uint64_t i = i0 + lane;
@@ -135,11 +143,16 @@ __global__ __launch_bounds__(64) void k_cls_count(
     for (int c = 0; c < kNumCls; ++c) cnt[c] += (uint32_t)__builtin_popcountll(__ballot(cls == c));
     nseg += wave_sum(nf);
     ntail += (uint32_t)__builtin_popcountll(__ballot(tail));
+    const int fb = cls == kClsLong ? fin_bucket(nf) : -1;
+#pragma unroll
+    for (int b = 0; b < kFinBuckets; ++b) fin[b] += (uint32_t)__builtin_popcountll(__ballot(fb == b));
   }
   if (lane < (uint32_t)kCols) {
     uint32_t v = lane == (uint32_t)kColSegs ? nseg : ntail;
 #pragma unroll
     for (int c = 0; c < kNumCls; ++c) v = lane == (uint32_t)c ? cnt[c] : v;
+#pragma unroll
+    for (int b = 0; b < kFinBuckets; ++b) v = lane == (uint32_t)(kColFin0 + b) ? fin[b] : v;
     part[(uint64_t)blockIdx.x * kCols + lane] = v;
   }
 }
@@ -170,7 +183,7 @@ __global__ __launch_bounds__(64) void k_cls_scatter(
     const noise_gpu_record *__restrict__ recs, uint64_t nrec, uint32_t chunk,
     uint32_t nkeys, const uint8_t *in, const uint8_t *out,
     const unsigned long long *wbase, RecHdr *hdr, uint32_t *idx, SegRec *rt,
-    SegEntry *segs, uint32_t *tails, uint64_t segcap) {
+    SegEntry *segs, uint32_t *tails, uint32_t *fin, uint64_t segcap) {
   const uint32_t lane = threadIdx.x;
   const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
   const uint64_t e0 = b0 + chunk < nrec ? b0 + chunk : nrec;
@@ -184,6 +197,15 @@ __global__ __launch_bounds__(64) void k_cls_scatter(
     for (int c = 0; c < kNumCls; ++c) {
       cbase[c] = b;
       b += hdr->counts[c];
+    }
+  }
+  unsigned long long fbase[kFinBuckets];
+  {
+    unsigned long long b = 0;
+#pragma unroll
+    for (int c = 0; c < kFinBuckets; ++c) {
+      fbase[c] = b;
+      b += hdr->counts[kColFin0 + c];
     }
   }
   if (blockIdx.x == 0 && lane < (uint32_t)kNumCls) {
@@ -216,6 +238,18 @@ __global__ __launch_bounds__(64) void k_cls_scatter(
         idx[cbase[c] + q] = (uint32_t)i;
       }
       run[c] += (unsigned long long)__builtin_popcountll(m);
+    }
+    {  // long records in finalize order: by segment-count bucket
+      const int fb = cls == kClsLong ? fin_bucket(nf) : -1;
+#pragma unroll
+      for (int b = 0; b < kFinBuckets; ++b) {
+        const uint64_t m = __ballot(fb == b);
+        if (fb == b)
+          fin[fbase[b] + run[kColFin0 + b] +
+              __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+              (uint32_t)q;
+        run[kColFin0 + b] += (unsigned long long)__builtin_popcountll(m);
+      }
     }
     {  // long records with a tail: the tail list (record order)
       const uint64_t m = __ballot(tail);
@@ -380,18 +414,23 @@ __global__ __launch_bounds__(64) void k_seg_tail(const uint32_t *__restrict__ ta
   }
 }
 
-// k_seg_finalize: lane per long record.  h = Horner over the segments'
-// partial sums in R = r^64, then h r^(tail blocks) + P_tail, the length
-// block and the tag.  Encrypt stores the tag; decrypt compares it and writes
-// the record's status.
+// k_seg_finalize: lane per long record, in finalize order (the classifier's
+// segment-count buckets: a wave's records loop over similar segment counts,
+// not up to the longest record of a random mix).  h = Horner over the
+// segments' partial sums in R = r^64, then h r^(tail blocks) + P_tail, the
+// length block and the tag.  Encrypt stores the tag; decrypt compares it and
+// writes the record's status.
 template <bool DECRYPT>
 __global__ __launch_bounds__(64) void k_seg_finalize(
-    const SegRec *__restrict__ rt, const SegPartial *__restrict__ partial,
-    const RecHdr *hdr, const uint8_t *in, uint8_t *out, uint8_t *status) {
-  const uint64_t n = hdr->nlong;
+    const uint32_t *__restrict__ fin, const SegRec *__restrict__ rt,
+    const SegPartial *__restrict__ partial, const RecHdr *hdr, const uint8_t *in, uint8_t *out,
+    uint8_t *status) {
+  const uint64_t n = hdr->counts[kClsLong], nlong = hdr->nlong;
 #pragma unroll 1
-  for (uint64_t q = (uint64_t)blockIdx.x * 64 + threadIdx.x; q < n;
-       q += (uint64_t)gridDim.x * 64) {
+  for (uint64_t t = (uint64_t)blockIdx.x * 64 + threadIdx.x; t < n;
+       t += (uint64_t)gridDim.x * 64) {
+    const uint32_t q = fin[t];
+    if (q >= nlong) continue;  // beyond the segment scratch: generic kernel
     const SegRec &R = rt[q];
     F26 R64, acc;
 #pragma unroll
@@ -401,8 +440,31 @@ __global__ __launch_bounds__(64) void k_seg_finalize(
       const SegPartial &P0 = partial[R.seg0];
       acc = to26(P0.h[0], P0.h[1], P0.h[2], P0.h[3], P0.h[4]);
     }
+    // Horner in R over the partial sums, 8 segments per step: the 8 loads
+    // are issued together (the loop is load-latency bound otherwise: one
+    // dependent round trip per segment, up to 63 per record)
+    uint32_t s = 1;
 #pragma unroll 1
-    for (uint32_t s = 1; s < nf; ++s) {
+    for (; s + 8 <= nf; s += 8) {
+      uint4 lo[8];
+      uint32_t hi[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const SegPartial &P = partial[R.seg0 + s + j];
+        lo[j] = make_uint4(P.h[0], P.h[1], P.h[2], P.h[3]);
+        hi[j] = P.h[4];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        acc = mul26(acc, R64);
+        const F26 t = to26(lo[j].x, lo[j].y, lo[j].z, lo[j].w, hi[j]);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) acc.a[i] += t.a[i];
+        carry26(acc);
+      }
+    }
+#pragma unroll 1
+    for (; s < nf; ++s) {
       const SegPartial &P = partial[R.seg0 + s];
       acc = mul26(acc, R64);
       const F26 t = to26(P.h[0], P.h[1], P.h[2], P.h[3], P.h[4]);
@@ -633,7 +695,8 @@ template <bool DECRYPT>
 static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr *hdr,
                                  const uint8_t *keys, uint32_t nkeys,
                                  const noise_gpu_record *recs, const uint32_t *idx,
-                                 const uint32_t *tails, uint64_t segbound, const uint8_t *in,
+                                 const uint32_t *tails, const uint32_t *fin, uint64_t segbound,
+                                 const uint8_t *in,
                                  uint8_t *out, const uint8_t *ad, uint8_t *status,
                                  hipStream_t stream) {
   AuxStream ax;
@@ -666,7 +729,7 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   const dim3 gseg(capped((segbound + 63) / 64, NOISE_GRID_CAP));
   hipLaunchKernelGGL((k_aead_tile<DECRYPT, 1024, false, kTileSeg>), gseg, bt, 0, stream, a);
   if ((e = hipStreamWaitEvent(stream, ax.join, 0)) != hipSuccess) return e;
-  hipLaunchKernelGGL((k_seg_finalize<DECRYPT>), grid, bt, 0, stream, ta.rt, ta.partial, hdr,
+  hipLaunchKernelGGL((k_seg_finalize<DECRYPT>), grid, bt, 0, stream, fin, ta.rt, ta.partial, hdr,
                      in, out, status);
   if (DECRYPT) {
     const dim3 gfix(capped((segbound + nrec + 63) / 64, NOISE_GRID_CAP));
@@ -700,12 +763,13 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   const uint64_t segcap = nrec * 63 < kSegCapMax ? nrec * 63 : kSegCapMax;
 
   // scratch: header | part[nw][kCols] | wbase[nw][kCols] | idx[nrec] |
-  //          tails[nrec] | rt[nrec] | segs[segcap] | partial[segcap]
+  //          tails[nrec] | fin[nrec] | rt[nrec] | segs[segcap] | partial[segcap]
   const uint64_t o_part = sizeof(RecHdr);
   const uint64_t o_wbase = align_up(o_part + nw * kCols * 4, 256);
   const uint64_t o_idx = align_up(o_wbase + nw * kCols * 8, 256);
   const uint64_t o_tails = align_up(o_idx + nrec * 4, 256);
-  const uint64_t o_rt = align_up(o_tails + nrec * 4, 256);
+  const uint64_t o_fin = align_up(o_tails + nrec * 4, 256);
+  const uint64_t o_rt = align_up(o_fin + nrec * 4, 256);
   const uint64_t o_segs = align_up(o_rt + nrec * sizeof(SegRec), 256);
   const uint64_t o_part2 = align_up(o_segs + segcap * sizeof(SegEntry), 256);
   const uint64_t bytes = o_part2 + segcap * sizeof(SegPartial);
@@ -718,6 +782,7 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   unsigned long long *wbase = reinterpret_cast<unsigned long long *>(base + o_wbase);
   uint32_t *idx = reinterpret_cast<uint32_t *>(base + o_idx);
   uint32_t *tails = reinterpret_cast<uint32_t *>(base + o_tails);
+  uint32_t *fin = reinterpret_cast<uint32_t *>(base + o_fin);
   SegRec *rt = reinterpret_cast<SegRec *>(base + o_rt);
   SegEntry *segs = reinterpret_cast<SegEntry *>(base + o_segs);
   SegPartial *partial = reinterpret_cast<SegPartial *>(base + o_part2);
@@ -725,7 +790,7 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   const dim3 b64(64);
   hipLaunchKernelGGL(k_cls_count, dim3((unsigned)nw), b64, 0, stream, recs, nrec, (uint32_t)chunk, nkeys, in, out, part);
   hipLaunchKernelGGL(k_cls_scan, dim3(kCols), b64, 0, stream, part, (uint32_t)nw, wbase, hdr, segcap);
-  hipLaunchKernelGGL(k_cls_scatter, dim3((unsigned)nw), b64, 0, stream, recs, nrec, (uint32_t)chunk, nkeys, in, out, wbase, hdr, idx, rt, segs, tails, segcap);
+  hipLaunchKernelGGL(k_cls_scatter, dim3((unsigned)nw), b64, 0, stream, recs, nrec, (uint32_t)chunk, nkeys, in, out, wbase, hdr, idx, rt, segs, tails, fin, segcap);
 
   TileArgs ta{};
   ta.in = in;
@@ -741,10 +806,10 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   ta.rt = rt;
   ta.partial = partial;
   ta.nseg = &hdr->nseg;
-  return decrypt ? launch_classes<true>(ta, nrec, hdr, keys, nkeys, recs, idx, tails, segcap, in,
-                                       out, ad, status, stream)
-                 : launch_classes<false>(ta, nrec, hdr, keys, nkeys, recs, idx, tails, segcap, in,
-                                         out, ad, status, stream);
+  return decrypt ? launch_classes<true>(ta, nrec, hdr, keys, nkeys, recs, idx, tails, fin, segcap,
+                                       in, out, ad, status, stream)
+                 : launch_classes<false>(ta, nrec, hdr, keys, nkeys, recs, idx, tails, fin, segcap,
+                                         in, out, ad, status, stream);
 }
 
 }  // namespace noise_amd

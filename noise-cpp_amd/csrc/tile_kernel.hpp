@@ -237,6 +237,36 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
 // compute (instead of after it), so it lands during the compute; the wave
 // then waits only for it (a counted vmcnt lets tile t-1's stores stay in
 // flight).  Twice the LDS: 33 KB per wave at L = 1024, one wave per SIMD.
+// kTileSeg: the per-lane metadata of one segment (from its SegRec)
+struct SegMeta {
+  uint32_t k[8], r[4], pw16[5], pw32[5];
+  uint32_t nlo, nhi, in_lo, in_hi, out_lo, out_hi, cb;
+};
+__device__ __forceinline__ void seg_meta_load(SegMeta &m, const SegRec *rt, const SegEntry e,
+                                              bool valid) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) m.k[i] = 0u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) m.r[i] = 0u;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) m.pw16[i] = m.pw32[i] = i == 0 ? 1u : 0u;
+  m.nlo = m.nhi = m.in_lo = m.in_hi = m.out_lo = m.out_hi = m.cb = 0u;
+  if (valid) {
+    const SegRec &R = rt[e.q];
+    const uint64_t io = R.in_off + 1024ull * e.s, oo = R.out_off + 1024ull * e.s;
+    m.in_lo = (uint32_t)io; m.in_hi = (uint32_t)(io >> 32);
+    m.out_lo = (uint32_t)oo; m.out_hi = (uint32_t)(oo >> 32);
+    m.nlo = (uint32_t)R.nonce; m.nhi = (uint32_t)(R.nonce >> 32);
+    m.cb = 16u * e.s;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) m.k[i] = R.k[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) m.r[i] = R.r[i];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) { m.pw16[i] = R.pw16[i]; m.pw32[i] = R.pw32[i]; }
+  }
+}
+
 template <bool DECRYPT, int L, bool CONTIG, int MODE = kTileUniform, int ABL = 0, int NBUF = 1,
           int SPAN = 256>
 __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
@@ -265,6 +295,19 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) gl[i] = swz(64u * i + lane) - 64u * i;
 
+  // kTileSeg: each super-tile's per-segment metadata (SegEntry -> SegRec,
+  // two dependent loads) is fetched one super-tile ahead -- the SegEntry with
+  // the current super-tile's first DMA, the SegRec fields once that DMA has
+  // landed -- so its latency hides behind the first tile's compute instead
+  // of stalling before every super-tile's first DMA.
+  SegMeta nxt;
+  SegEntry nxt_e{0u, 0u};
+  if (SEG) {
+    const uint64_t g = (uint64_t)blockIdx.x * 64 + lane;
+    if (g < nrec) nxt_e = a.segs[g];
+    seg_meta_load(nxt, a.rt, nxt_e, g < nrec);
+  }
+
 #pragma unroll 1
   for (uint64_t super0 = (uint64_t)blockIdx.x * 64; super0 < nrec;
        super0 += (uint64_t)gridDim.x * 64) {
@@ -275,39 +318,26 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
   uint32_t own_in_lo = 0, own_in_hi = 0, own_out_lo = 0, own_out_hi = 0, own_di = 0;
   uint32_t own_cb = 0;  // kTileSeg: first ChaCha block counter - 1 (16 s)
   bool own_bad = false, own_inplace = false;
+  const uint64_t next0 = super0 + (uint64_t)gridDim.x * 64;  // kTileSeg prefetch
   if (SEG) {
-    const uint64_t g = super0 + lane;
-    uint64_t n = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) own_k[i] = 0u;
+    for (int i = 0; i < 8; ++i) own_k[i] = nxt.k[i];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) kr[i] = kss[i] = 0u;
+    for (int i = 0; i < 4; ++i) { kr[i] = nxt.r[i]; kss[i] = 0u; }
 #pragma unroll
-    for (int b = 0; b < (C::LOG2G > 0 ? C::LOG2G : 1); ++b)
-#pragma unroll
-      for (int i = 0; i < 5; ++i) pw[b].a[i] = i == 0 ? 1u : 0u;
-    if (g < nrec) {
-      const SegEntry e = a.segs[g];
-      const SegRec &R = a.rt[e.q];
-      n = R.nonce;
-      const uint64_t io = R.in_off + 1024ull * e.s, oo = R.out_off + 1024ull * e.s;
-      own_in_lo = (uint32_t)io; own_in_hi = (uint32_t)(io >> 32);
-      own_out_lo = (uint32_t)oo; own_out_hi = (uint32_t)(oo >> 32);
-      own_cb = 16u * e.s;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) own_k[i] = R.k[i];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) { kr[i] = R.r[i]; kss[i] = 0u; }
-#pragma unroll
-      for (int i = 0; i < 5; ++i) { pw[0].a[i] = R.pw16[i]; pw[C::LOG2G > 1 ? 1 : 0].a[i] = R.pw32[i]; }
-    }
-    own_nlo = (uint32_t)n;
-    own_nhi = (uint32_t)(n >> 32);
+    for (int i = 0; i < 5; ++i) { pw[0].a[i] = nxt.pw16[i]; pw[C::LOG2G > 1 ? 1 : 0].a[i] = nxt.pw32[i]; }
+    own_nlo = nxt.nlo;
+    own_nhi = nxt.nhi;
+    own_in_lo = nxt.in_lo; own_in_hi = nxt.in_hi;
+    own_out_lo = nxt.out_lo; own_out_hi = nxt.out_hi;
+    own_cb = nxt.cb;
     const uint64_t left = nrec - super0;
     tile_load<L, DECRYPT, CONTIG, MODE, ABL, SPAN>(
         NOISE_LDS3(lds), in, a.in_stride, super0,
         left < (uint64_t)C::RPT ? (uint32_t)left : C::RPT, lane, gl, 0u,
         own_in_lo, own_in_hi);
+    nxt_e = SegEntry{0u, 0u};
+    if (next0 + lane < nrec) nxt_e = a.segs[next0 + lane];
   } else {
     uint64_t n = a.nonce0 + super0 + lane;
     if (KEYED) {
@@ -383,6 +413,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     if (NBUF == 2 && prev_all) wait_vmcnt<NOUT>();
     else wait_vmem();
     wave_lds_fence();
+    if (SEG && t == 0) seg_meta_load(nxt, a.rt, nxt_e, next0 + lane < nrec);
     if (NBUF == 2 && t + 1 < C::G) {  // the next tile's DMA now, into the other buffer
       const uint64_t nrec0 = rec0 + C::RPT;
       if (nrec0 < nrec) {

@@ -10,7 +10,7 @@
 //   2. one launch per class, each reading its slice and count from device
 //      memory:
 //        - tile classes: 16-byte aligned, AD-free records of 64, 128, 192,
-//          256, 512 bytes -> the LDS-staged tile kernel (tile_kernel.hpp,
+//          256, 512, 1024 bytes -> the LDS-staged tile kernel (tile_kernel.hpp,
 //          kTileDesc);
 //        - long records: 16-byte aligned, AD-free, 1024 <= len <= 65535
 //          (any length) -> cut into 1 KiB segments + a tail.  k_seg_prep
@@ -37,7 +37,7 @@
 namespace noise_amd {
 
 constexpr int kGenBlock = 256;
-constexpr int kNumTileCls = 5;            // 64 128 192 256 512
+constexpr int kNumTileCls = 6;            // 64 128 192 256 512 1024
 constexpr int kClsLong = kNumTileCls;     // segmented long records
 constexpr int kClsGeneric = kNumTileCls + 1;
 constexpr int kNumCls = kNumTileCls + 2;
@@ -77,6 +77,7 @@ __device__ __forceinline__ int record_class(const noise_gpu_record &d,
     case 192: return 2;
     case 256: return 3;
     case 512: return 4;
+    case 1024: return 5;  // exactly 1 KiB: one tile-kernel pass beats prep + segment + finalize
     default: break;
   }
   return (d.len >= 1024u && d.len <= kLongMax) ? kClsLong : kClsGeneric;
@@ -105,6 +106,18 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
   for (int d = 1; d < 64; d <<= 1) {
     const uint32_t t = (uint32_t)__shfl((int)v, (int)(lane >= (uint32_t)d ? lane - d : lane));
     if (lane >= (uint32_t)d) v += t;
+  }
+  return v;
+}
+
+__device__ __forceinline__ unsigned long long wave_incl_scan64(unsigned long long v,
+                                                               uint32_t lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int src = (int)(lane >= (uint32_t)d ? lane - d : lane);
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
+    if (lane >= (uint32_t)d) v += ((unsigned long long)hi << 32) | lo;
   }
   return v;
 }
@@ -157,21 +170,32 @@ __global__ __launch_bounds__(64) void k_cls_count(
   }
 }
 
-// one workgroup per column
+// one workgroup per column.  Lane l owns the contiguous waves
+// [l*per, (l+1)*per): all its loads go out together (one memory round trip
+// instead of one per 64 waves), then a local prefix, a wave scan of the lane
+// totals, and the bases are written back.
 __global__ __launch_bounds__(64) void k_cls_scan(const uint32_t *part, uint32_t nw,
                                                  unsigned long long *wbase,
                                                  RecHdr *hdr, uint64_t segcap) {
   const uint32_t lane = threadIdx.x, c = blockIdx.x;
-  unsigned long long run = 0;
-#pragma unroll 1
-  for (uint32_t w0 = 0; w0 < nw; w0 += 64) {
-    const uint32_t w = w0 + lane;
-    const uint32_t v = w < nw ? part[(uint64_t)w * kCols + c] : 0u;
-    const uint32_t inc = wave_incl_scan(v, lane);
-    if (w < nw) wbase[(uint64_t)w * kCols + c] = run + inc - v;
-    run += (uint32_t)__shfl((int)inc, 63);
+  constexpr uint32_t kPer = 32;  // nw <= 2048 (the classifier's geometry)
+  const uint32_t w0 = lane * kPer;
+  uint32_t v[kPer];
+  unsigned long long tot = 0;  // 32 waves' segment counts can pass 2^32
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) {
+    v[i] = w0 + i < nw ? part[(uint64_t)(w0 + i) * kCols + c] : 0u;
   }
-  if (lane == 0) {
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) tot += v[i];
+  const unsigned long long inc = wave_incl_scan64(tot, lane);
+  unsigned long long run = inc - tot;
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) {
+    if (w0 + i < nw) wbase[(uint64_t)(w0 + i) * kCols + c] = run;
+    run += v[i];
+  }
+  if (lane == 63) {
     hdr->counts[c] = run;
     // lowered by k_cls_scatter if the segment scratch overflows
     if (c == (uint32_t)kClsLong) hdr->nlong = run;
@@ -719,6 +743,7 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   NOISE_DESC_TILE(2, 192)
   NOISE_DESC_TILE(3, 256)
   NOISE_DESC_TILE(4, 512)
+  NOISE_DESC_TILE(5, 1024)
 #undef NOISE_DESC_TILE
   const uint64_t gblocks = (nrec + kGenBlock - 1) / kGenBlock;
   const dim3 gg((unsigned)(gblocks < 2 * NOISE_GRID_CAP ? gblocks : 2 * NOISE_GRID_CAP));

@@ -179,10 +179,11 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
           lds_dma16_s(base, 16u * (r * (C::SPR + 1) + C::SPR), (lds_void *)(lds3 + 64 * q));
       }
     }
-  } else if (MODE == kTileSeg) {
-    // 1 KiB segments: DMA instruction q moves all 64 pieces of segment q, so
-    // its offset is wave-uniform -- read from the segment's key lane
-    // (v_readlane into SGPRs) instead of a per-lane shuffle
+  } else if (MODE == kTileSeg || (MODE == kTileDesc && C::SPR == 64)) {
+    // 1 KiB units (segments, or kTileDesc records of exactly 1 KiB): DMA
+    // instruction q moves all 64 pieces of unit q, so its offset is
+    // wave-uniform -- read from the unit's key lane (v_readlane into SGPRs)
+    // instead of a per-lane shuffle
 #pragma unroll
     for (int q = 0; q < C::RPT; ++q) {
       if ((uint32_t)q < nv) {
@@ -191,6 +192,13 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
                                     (uint32_t)__builtin_amdgcn_readlane((int)own_in_lo, (int)kl));
         lds_dma16_s(in + off, 16u * gl[q & 3], (lds_void *)(lds3 + 64 * q));
       }
+    }
+    if (TAGGED_IN) {  // decrypt: the RPT tags, lane r -> slot REC_SLOTS + r
+      const uint32_t r = lane < (uint32_t)C::RPT ? lane : 0u;
+      const uint64_t off = ((uint64_t)(uint32_t)__shfl((int)own_in_hi, (int)(t_rpt + r)) << 32) |
+                           (uint32_t)__shfl((int)own_in_lo, (int)(t_rpt + r));
+      if (lane < (uint32_t)C::RPT && lane < nv)
+        lds_dma16_v(in + off + 16u * C::SPR, (lds_void *)(lds3 + C::REC_SLOTS));
     }
   } else {
 #pragma unroll 1
@@ -551,73 +559,113 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     const uint64_t inpl_mask = MODE == kTileDesc ? __ballot(j == 0 && rec_inplace) : 0ull;
     wave_lds_fence();
 
-    // ---- gather this tile's output records into registers ----------------
-    uint4 ov[NOUT];
-    bool st[NOUT];
+    // ---- gather this tile's output records into registers, store them --
+    // Keyed modes gather and store in NPART parts: 17 uint4 pieces live at
+    // once (L >= 512 encrypt) push those kernels past 256 VGPRs into AGPR
+    // and SGPR spills.  The next tile's DMA overwrites the LDS, so it goes
+    // out after the last part's gather (before that part's stores).
+    constexpr int NPART = (KEYED && NBUF == 1 && NOUT > 8) ? 2 : 1;
+    constexpr int NQ = (NOUT + NPART - 1) / NPART;
     const bool full = nv == (uint32_t)C::RPT;
-#pragma unroll
-    for (int q = 0; q < NOUT; ++q) {
+    // RECQ (1 KiB units: segments, 1 KiB descriptor records): output
+    // instruction q < RPT holds the 64 data pieces of record q (uniform
+    // destination, v_readlane), instruction RPT (encrypt) the RPT tags
+    constexpr bool RECQ = SEG || (MODE == kTileDesc && C::SPR == 64);
+    auto piece = [&](int q, uint32_t &r, uint32_t &pc, uint32_t &slot, bool &ok) {
+      if (RECQ) {
+        if (q < C::RPT) {
+          r = (uint32_t)q; pc = lane; slot = swz(64u * q + lane); ok = true;
+        } else {
+          r = lane < (uint32_t)C::RPT ? lane : 0u; pc = C::SPR; slot = C::REC_SLOTS + r;
+          ok = lane < (uint32_t)C::RPT;
+        }
+        return;
+      }
       const uint32_t g = 64u * q + lane;  // output piece (record r, piece pc)
-      const uint32_t r = g / OPR, pc = g % OPR;
-      uint32_t slot;
+      r = g / OPR;
+      pc = g % OPR;
       if (CONTIG && DECRYPT) slot = 64u * q + gl[q & 3];  // == swz(g)
       else slot = pc < (uint32_t)C::SPR ? swz(r * C::SPR + pc) : C::REC_SLOTS + r;
-      st[q] = (OUT_SLOTS % 64 == 0 || g < (uint32_t)OUT_SLOTS) && (full || r < nv);
-      ov[q] = lb[slot < (uint32_t)C::NSLOT ? slot : 0u];
-    }
-    // Records that must not be output as computed (rare; a separate,
-    // wave-uniform branch so the common path carries none of this):
-    // failed tag (decrypt): keep an in-place record, zero a copy; invalid key
-    // index: write nothing.
-    if ((DECRYPT || KEYED) && fail_mask != 0) {
+      ok = OUT_SLOTS % 64 == 0 || g < (uint32_t)OUT_SLOTS;
+    };
 #pragma unroll
-      for (int q = 0; q < NOUT; ++q) {
-        const uint32_t r = (64u * q + lane) / OPR;
-        if ((fail_mask >> (r * C::G)) & 1u) {
-          const bool bad_key_rec = KEYED && ((badk_mask >> (r * C::G)) & 1u);
-          const bool inpl = MODE == kTileDesc ? ((inpl_mask >> (r * C::G)) & 1u) != 0
-                                              : a.in_place != 0;
-          st[q] = st[q] && DECRYPT && !inpl && !bad_key_rec;
-          ov[q] = make_uint4(0u, 0u, 0u, 0u);
+    for (int part = 0; part < NPART; ++part) {
+      const int q0 = part * NQ;
+      uint4 ov[NQ];
+      bool st[NQ];
+#pragma unroll
+      for (int qq = 0; qq < NQ; ++qq) {
+        const int q = q0 + qq;
+        if (q >= NOUT) break;
+        uint32_t r, pc, slot;
+        bool ok;
+        piece(q, r, pc, slot, ok);
+        st[qq] = ok && (full || r < nv);
+        ov[qq] = lb[slot < (uint32_t)C::NSLOT ? slot : 0u];
+      }
+      // Records that must not be output as computed (rare; a separate,
+      // wave-uniform branch so the common path carries none of this):
+      // failed tag (decrypt): keep an in-place record, zero a copy; invalid
+      // key index: write nothing.
+      if ((DECRYPT || KEYED) && fail_mask != 0) {
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq) {
+          const int q = q0 + qq;
+          if (q >= NOUT) break;
+          uint32_t r, pc, slot;
+          bool ok;
+          piece(q, r, pc, slot, ok);
+          if ((fail_mask >> (r * C::G)) & 1u) {
+            const bool bad_key_rec = KEYED && ((badk_mask >> (r * C::G)) & 1u);
+            const bool inpl = MODE == kTileDesc ? ((inpl_mask >> (r * C::G)) & 1u) != 0
+                                                : a.in_place != 0;
+            st[qq] = st[qq] && DECRYPT && !inpl && !bad_key_rec;
+            ov[qq] = make_uint4(0u, 0u, 0u, 0u);
+          }
         }
       }
-    }
-    wait_lds();  // LDS reads done
-    wave_lds_fence();
-
-    // ---- NBUF = 1: next tile's DMA, then this tile's stores, both in flight
-    if (NBUF == 1 && t + 1 < C::G) {
-      const uint64_t nrec0 = rec0 + C::RPT;
-      if (nrec0 < nrec) {
-        const uint64_t left = nrec - nrec0;
-        tile_load<L, DECRYPT, CONTIG, MODE, ABL, SPAN>(
-            NOISE_LDS3(lds), in, a.in_stride, nrec0,
-            left < (uint64_t)C::RPT ? (uint32_t)left : C::RPT, lane, gl,
-            (uint32_t)(t + 1) * C::RPT, own_in_lo, own_in_hi);
+      if (part == NPART - 1) {
+        wait_lds();  // LDS reads done
+        wave_lds_fence();
+        // ---- NBUF = 1: next tile's DMA, then these stores, both in flight
+        if (NBUF == 1 && t + 1 < C::G) {
+          const uint64_t nrec0 = rec0 + C::RPT;
+          if (nrec0 < nrec) {
+            const uint64_t left = nrec - nrec0;
+            tile_load<L, DECRYPT, CONTIG, MODE, ABL, SPAN>(
+                NOISE_LDS3(lds), in, a.in_stride, nrec0,
+                left < (uint64_t)C::RPT ? (uint32_t)left : C::RPT, lane, gl,
+                (uint32_t)(t + 1) * C::RPT, own_in_lo, own_in_hi);
+          }
+        }
       }
-    }
 #pragma unroll
-    for (int q = 0; q < NOUT; ++q) {
-      const uint32_t g = 64u * q + lane;
-      const uint32_t r = g / OPR, pc = g % OPR;
-      bool store = st[q];
-      if (ABL == 1) store = store && (ov[q].x == 0x12345678u && ov[q].y == 0x9abcdef0u);
-      uint8_t *dst;
-      if (SEG) {  // output instruction q = segment q (OPR = 64): uniform offset
-        const uint32_t kl = (uint32_t)t * C::RPT + (uint32_t)q;
-        const uint64_t off = join64((uint32_t)__builtin_amdgcn_readlane((int)own_out_hi, (int)kl),
-                                    (uint32_t)__builtin_amdgcn_readlane((int)own_out_lo, (int)kl));
-        dst = out + off + 16u * pc;
-      } else if (MODE == kTileDesc) {
-        const uint32_t rs = (uint32_t)t * C::RPT + (r < (uint32_t)C::RPT ? r : 0u);
-        const uint64_t off = ((uint64_t)(uint32_t)__shfl((int)own_out_hi, rs) << 32) |
-                             (uint32_t)__shfl((int)own_out_lo, rs);
-        dst = out + off + 16u * pc;
-      } else {
-        dst = out + rec0 * a.out_stride +
-              (CONTIG ? 16ull * g : r * a.out_stride + 16u * pc);
+      for (int qq = 0; qq < NQ; ++qq) {
+        const int q = q0 + qq;
+        if (q >= NOUT) break;
+        const uint32_t g = 64u * q + lane;
+        uint32_t r, pc, slot;
+        bool ok;
+        piece(q, r, pc, slot, ok);
+        bool store = st[qq];
+        if (ABL == 1) store = store && (ov[qq].x == 0x12345678u && ov[qq].y == 0x9abcdef0u);
+        uint8_t *dst;
+        if (RECQ && q < C::RPT) {  // output instruction q = record / segment q: uniform offset
+          const uint32_t kl = (uint32_t)t * C::RPT + (uint32_t)q;
+          const uint64_t off = join64((uint32_t)__builtin_amdgcn_readlane((int)own_out_hi, (int)kl),
+                                      (uint32_t)__builtin_amdgcn_readlane((int)own_out_lo, (int)kl));
+          dst = out + off + 16u * pc;
+        } else if (MODE == kTileDesc) {
+          const uint32_t rs = (uint32_t)t * C::RPT + (r < (uint32_t)C::RPT ? r : 0u);
+          const uint64_t off = ((uint64_t)(uint32_t)__shfl((int)own_out_hi, rs) << 32) |
+                               (uint32_t)__shfl((int)own_out_lo, rs);
+          dst = out + off + 16u * pc;
+        } else {
+          dst = out + rec0 * a.out_stride +
+                (CONTIG ? 16ull * g : r * a.out_stride + 16u * pc);
+        }
+        if (store) store16<true>(dst, ov[qq], 16);
       }
-      if (store) store16<true>(dst, ov[q], 16);
     }
     prev_all = ABL == 0 && full && fail_mask == 0;
   }

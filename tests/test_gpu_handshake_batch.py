@@ -168,3 +168,61 @@ def test_batch_message_length_checks():
     assert all(s[i] == 0 for i in range(n) if i not in bad)
     I.close()
     R.close()
+
+
+def test_batch_api_rules_and_shared_static_key():
+    """Host-side rules of the batched API (turn order, keys before start, psk
+    count, finished/split order) and a stride-0 static key (one server key for
+    every session, derived once and broadcast) giving the same handshakes as
+    the same key installed per session."""
+    n = 130
+    E = noise_amd.NoiseGpuError
+    rng = np.random.default_rng(3)
+    srv = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+    cli = [bytes(rng.integers(0, 256, 32, dtype=np.uint8)) for _ in range(n)]
+    eph = [[bytes(rng.integers(0, 256, 32, dtype=np.uint8)) for _ in range(n)] for _ in range(2)]
+    results = []
+    for shared in (True, False):
+        I, R = noise_amd.HandshakeBatch("XX", True, n), noise_amd.HandshakeBatch("XX", False, n)
+        I.set_key(noise_amd.HS_S, _dev(b"".join(cli)))
+        I.set_key(noise_amd.HS_E, _dev(b"".join(eph[0])))
+        if shared:
+            R.set_key(noise_amd.HS_S, _dev(srv), stride=0)
+        else:
+            R.set_key(noise_amd.HS_S, _dev(srv * n))
+        R.set_key(noise_amd.HS_E, _dev(b"".join(eph[1])))
+        buf = torch.zeros(n * 128, dtype=torch.uint8, device="cuda")
+        with pytest.raises(E):  # not started
+            I.write_message(noise_amd.span(buf, stride=128))
+        I.start()
+        R.start()
+        with pytest.raises(E):  # keys go in before start
+            I.set_key(noise_amd.HS_S, _dev(b"".join(cli)))
+        with pytest.raises(E):  # the responder reads first
+            R.write_message(noise_amd.span(buf, stride=128))
+        with pytest.raises(E):  # not finished
+            I.split(*(torch.zeros(32 * n, dtype=torch.uint8, device="cuda") for _ in range(2)))
+        msgs = []
+        for m in range(3):
+            w, r = (I, R) if m % 2 == 0 else (R, I)
+            ov = w.info().overhead
+            w.write_message(noise_amd.span(buf, stride=128))
+            r.read_message(noise_amd.span(buf, stride=128, length=ov))
+            msgs.append(buf.view(n, 128)[:, :ov].cpu().numpy().copy())
+        assert I.info().finished == 1 and R.info().my_turn == 0
+        with pytest.raises(E):  # finished
+            I.write_message(noise_amd.span(buf, stride=128))
+        k = [torch.zeros(32 * n, dtype=torch.uint8, device="cuda") for _ in range(4)]
+        I.split(k[0], k[1])
+        R.split(k[2], k[3])
+        torch.cuda.synchronize()
+        assert torch.equal(k[0], k[2]) and torch.equal(k[1], k[3])
+        results.append((msgs, k[0].cpu().numpy()))
+        I.close()
+        R.close()
+    for a, b in zip(results[0][0], results[1][0]):
+        assert np.array_equal(a, b)
+    assert np.array_equal(results[0][1], results[1][1])
+    with pytest.raises(E):  # psk pattern without psks
+        P = noise_amd.HandshakeBatch("NNpsk0", True, 4)
+        P.start()

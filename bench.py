@@ -10,30 +10,48 @@ two kernel launches on one HIP stream.  `value` counts plaintext bytes through
 the AEAD (encrypt + decrypt) of all ranks / wall time of the K timed steps
 (max over ranks), in GiB/s (2^30 B/s).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
-                    [--no-cpu-baseline] [--host-inclusive]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1|2|3|4|5]
+                    [--no-cpu-baseline] [--no-config1] [--host-inclusive]
 
-N > 1 is launched by torch.distributed.run, one process per GPU; records are
-sharded per GPU with no data-path collective (weak scaling: each rank owns
-its own R records and nonce range).  torch.distributed (RCCL) is used only
-for the barrier and the max-over-ranks of the elapsed time.
+Multi-GPU: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set)
+each process is one rank.  Run directly with --gpus N > 1, this process is
+only a launcher: before touching any GPU it starts N copies of itself with
+RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set and
+exits with their status; rank 0 prints the JSON line.  Records shard per GPU
+with no data-path collective (cfg 2/3/4 weak scaling: each rank its own R
+records and nonce range; cfg 5 strong scaling: one 8 Mi-record range cut in
+contiguous slices).  torch.distributed (RCCL) carries only the barrier, the
+max-over-ranks of the elapsed time and the per-rank shard table.
+
+--stub (tests only, CPU): the same launcher, rank bookkeeping, barriers and
+reductions over gloo, with a trivial host workload instead of the GPU.
 """
 import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "noise-cpp_amd", "python"))
 
-import noise_amd  # noqa: E402
+import noise_amd  # noqa: E402  (lazy: loads the library on first use)
 
 SEED = 0x4E4F495345
 KEY = bytes(range(32))
 HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md)
+# VALU issue roof: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 4
+# cycles per SIMD at the 2.4 GHz max clock.  4 cycles is the measured cost of
+# every instruction in a ChaCha / Poly1305 stream on gfx950 (alignbit,
+# mad_u64_u32, add_co: "slow" class; a stream mixing them with the 2-cycle
+# add/xor runs all of it at ~4 cycles: profiles/round2/issue_bench.txt,
+# profiles/round2/valu_classes.txt, DESIGN.md section 4.2).
+VALU_PEAK = 1024 * 2.4e9 / 4.0  # wave-instructions / s
 GIB = float(1 << 30)
+SHARE_CPUS = 16  # host CPU share of one GPU on the GPU box
 
 
 def log(msg):
@@ -48,9 +66,9 @@ def shard(total, rank, world):
 def rank_nonce_base(cfg, rank, world, per_rank, total):
     """First nonce of a rank's records: weak scaling (cfg 2) gives every rank
     its own R-record nonce range; strong scaling (cfg 5) splits one range."""
-    if cfg == 2:
-        return rank * per_rank
-    return shard(total, rank, world)[0]
+    if cfg == 5:
+        return shard(total, rank, world)[0]
+    return rank * per_rank
 
 
 def reduce_over_ranks(dist, elapsed, nrec, device):
@@ -63,61 +81,141 @@ def reduce_over_ranks(dist, elapsed, nrec, device):
     return float(t.item()), int(n.item())
 
 
-def pmc_traffic(workload):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any
-    (profiles/*/pmc_traffic.json, written from a separate --pmc pass)."""
-    best = None
+def check_shards(shards):
+    """Rank shard table -> error text if two ranks share a nonce."""
+    spans = sorted((s["nonce_lo"], s["nonce_hi"], s["rank"]) for s in shards)
+    for a, b in zip(spans, spans[1:]):
+        if b[0] < a[1]:
+            return "ranks %d and %d share nonces [%d, %d)" % (a[2], b[2], b[0], min(a[1], b[1]))
+    return None
+
+
+# ---------------------------------------------------------------- launcher
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch(args, argv):
+    """--gpus N > 1 without WORLD_SIZE: start N ranks of this script (one per
+    GPU) and return their worst exit status.  Nothing here touches a GPU:
+    torch.cuda.device_count() does not initialise the device on this image."""
+    n = args.gpus
+    if not args.stub:
+        import torch
+        have = torch.cuda.device_count()
+        if have < n:
+            raise SystemExit("bench.py --gpus %d: only %d GPU(s) visible" % (n, have))
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                log("a rank exited with status %d; stopping the others" % code)
+                for q in pending:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+# ---------------------------------------------------------------- profiles
+def latest_profile(cfg):
+    """Per-kernel PMC means of the newest committed profile of config `cfg`
+    (profiles/roundNN/cfgN/pmc_summary.json, tools/gpu/profile_cfg.sh)."""
     pdir = os.path.join(ROOT, "profiles")
+    best = None
     if os.path.isdir(pdir):
         for sub in sorted(os.listdir(pdir)):
-            f = os.path.join(pdir, sub, "pmc_traffic.json")
+            f = os.path.join(pdir, sub, "cfg%d" % cfg, "pmc_summary.json")
             if os.path.exists(f):
-                d = json.load(open(f))
-                if d.get("workload") == workload:
-                    best = d
+                best = (os.path.relpath(f, ROOT), json.load(open(f)))
     return best
 
 
-def cpu_baseline(seconds=1.5, threads=None):
-    """Reference monocypher.c (oracle/_ref) -- or the build's C restatement
-    if _ref is absent -- on this host's cores: 1 KiB records, encrypt +
-    decrypt, repeated passes of 2^15 records until `seconds` of wall time."""
+def pmc_kernels(prof, names):
+    """Sum the per-dispatch PMC means of the kernels whose symbol starts with
+    one of `names` (one launch each per call)."""
+    if not prof:
+        return None
+    ks = prof[1]["kernels"]
+    rows = [v for k, v in ks.items() if any(k.startswith(n) for n in names)]
+    if not rows:
+        return None
+    out = {}
+    for r in rows:
+        for c, v in r.items():
+            out[c] = out.get(c, 0.0) + v
+    return out
+
+
+# ---------------------------------------------------------------- cpu leg
+def cpu_baseline(threads=None):
+    """Reference monocypher.c (oracle/_ref, the reference's own source built
+    by oracle/Makefile) -- or the build's C restatement if _ref is absent --
+    on this host's cores, BASELINE.md section 3: 1 KiB records, encrypt and
+    decrypt separately, at 1 thread and at the GPU's host CPU share, plus a
+    1 -> N thread encrypt line.  A bounded sample: 2^15 records per pass,
+    repeated until each figure has ~0.4-1.5 s of wall time (~15 s in all)."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
     orc = oracle_lib.Oracle()
-    threads = threads or min(16, os.cpu_count() or 1)
+    ncpu = os.cpu_count() or 1
+    threads = threads or min(SHARE_CPUS, ncpu)
     L, R = 1024, 1 << 15
     pt = np.frombuffer(orc.synthetic(R * L, SEED), dtype=np.uint8).copy()
     ct = np.zeros(R * (L + 16), dtype=np.uint8)
     back = np.zeros(R * L, dtype=np.uint8)
-    if orc.ref is not None:
-        kind = "reference"
-        fails = ctypes.c_int(0)
+    kind = "reference" if orc.ref is not None else "port"
+    fails = ctypes.c_int(0)
 
-        def run(dec):
+    def run(dec, nthr):
+        if orc.ref is not None:
             if dec:
                 return orc.ref.ref_batch_uniform(1, KEY, 0, ct.ctypes.data, L + 16, back.ctypes.data,
-                                                 L, L, R, threads, ctypes.byref(fails))
+                                                 L, L, R, nthr, ctypes.byref(fails))
             return orc.ref.ref_batch_uniform(0, KEY, 0, pt.ctypes.data, L, ct.ctypes.data, L + 16,
-                                             L, R, threads, ctypes.byref(fails))
-    else:
-        kind = "port"
+                                             L, R, nthr, ctypes.byref(fails))
+        if dec:
+            return orc.lib.oracle_batch_uniform(1, KEY, 0, ct.ctypes.data, L + 16, back.ctypes.data,
+                                                L, L, R, nthr, None)
+        return orc.lib.oracle_batch_uniform(0, KEY, 0, pt.ctypes.data, L, ct.ctypes.data, L + 16,
+                                            L, R, nthr, None)
 
-        def run(dec):
-            if dec:
-                return orc.lib.oracle_batch_uniform(1, KEY, 0, ct.ctypes.data, L + 16,
-                                                    back.ctypes.data, L, L, R, threads, None)
-            return orc.lib.oracle_batch_uniform(0, KEY, 0, pt.ctypes.data, L, ct.ctypes.data,
-                                                L + 16, L, R, threads, None)
-    run(False)  # warm
-    t = 0.0
-    passes = 0
-    while t < seconds:
-        t += run(False) + run(True)
-        passes += 1
-    assert np.array_equal(pt, back), "cpu baseline round trip failed"
-    value = passes * 2 * R * L / t / GIB
+    def rate(dec, nthr, seconds):
+        run(dec, nthr)  # warm
+        t, passes = 0.0, 0
+        while t < seconds:
+            t += run(dec, nthr)
+            passes += 1
+        return passes * R * L / t / GIB
+
+    enc1 = rate(False, 1, 1.5)
+    dec1 = rate(True, 1, 1.5)
+    encn = rate(False, threads, 1.0)
+    decn = rate(True, threads, 1.0)
+    assert np.array_equal(pt, back) and fails.value == 0, "cpu baseline round trip failed"
+    scaling = {}
+    t = 1
+    while t <= threads:
+        scaling[str(t)] = round(enc1 if t == 1 else encn if t == threads else rate(False, t, 0.4), 3)
+        t *= 2
+    if str(threads) not in scaling:
+        scaling[str(threads)] = round(encn, 3)
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -126,127 +224,59 @@ def cpu_baseline(seconds=1.5, threads=None):
                 break
     except OSError:
         pass
+    value = 2.0 / (1.0 / encn + 1.0 / decn)  # enc+dec round trip, like `value`
     return {"value": round(value, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-            "sample": "%d passes x %d x 1 KiB records encrypt+decrypt (%.1f s wall, %d threads, "
-                      "%s, CPU %s)" % (passes, R, t, threads,
-                                       "monocypher.c via oracle/_ref" if kind == "reference"
-                                       else "oracle/chachapoly_oracle.c", model)}
+            "encrypt_GiBps": {"1": round(enc1, 3), str(threads): round(encn, 3)},
+            "decrypt_GiBps": {"1": round(dec1, 3), str(threads): round(decn, 3)},
+            "encrypt_thread_scaling_GiBps": scaling,
+            "cpu_model": model, "nproc": ncpu,
+            "sample": "1 KiB records, 2^15 per pass, encrypt and decrypt timed separately "
+                      "(1 thread ~1.5 s each, %d threads ~1 s each, scaling points ~0.4 s); value = "
+                      "enc+dec rate at %d threads (the GPU's host CPU share; nproc reports %d); %s"
+                      % (threads, threads, ncpu, "monocypher.c via oracle/_ref" if kind == "reference"
+                         else "oracle/chachapoly_oracle.c")}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--min-warmup-s", type=float, default=0.3,
-                    help="keep running untimed warmup steps until this much wall time has passed "
-                         "(the GPU clock ramps over ~0.1 s; see DESIGN.md)")
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
-    ap.add_argument("--records", type=int, default=0, help="override records per GPU")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--host-inclusive", action="store_true",
-                    help="also time the pinned-host H2D->kernel->D2H pipeline (DESIGN.md)")
-    args = ap.parse_args()
-
-    import torch
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    noise_amd.load()
-    stream = torch.cuda.current_stream()
-
-    cfg = args.config
-    wl = make_workload(cfg, args, rank, world, stream)
-    R, L, workload, step = wl["R"], wl["L"], wl["workload"], wl["step"]
-
-    log("rank %d/%d: %d records x %d B, warmup %d" % (rank, world, R, L, args.warmup))
-    # correctness of the step about to be timed: all tags verify, round trip
-    # exact (checked before the warmup so no host-side idle gap -- during which
-    # the GPU clock drops -- separates the warmup from the timed steps)
-    step()
-    torch.cuda.synchronize()
-    if not wl["check"]():
-        raise SystemExit("round trip failed on rank %d" % rank)
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    tw = time.perf_counter()
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    while time.perf_counter() - tw < args.min_warmup_s:
-        for _ in range(4):
-            step()
-        torch.cuda.synchronize()
-
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(evs[i])
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        elapsed, total_rec = reduce_over_ranks(dist, elapsed, R, "cuda")
-    else:
-        total_rec = R
-    # the timed work was correct too
-    if not wl["check"]():
-        raise SystemExit("timed round trip failed on rank %d" % rank)
-    enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
-    dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
-    log("enc %.3f ms, dec %.3f ms per launch; step %.3f ms" %
-        (enc_ms, dec_ms, elapsed * 1e3 / args.steps))
-
-    # plaintext through the AEAD (enc + dec), scaled from this rank's records
-    total_bytes = 2.0 * wl["pt_bytes"] * (total_rec / R) * args.steps
-    value = total_bytes / elapsed / GIB
-
-    # roofline of the dominant kernel (algorithmic bytes per launch / its
-    # average duration from the HIP events on its own stream)
-    enc_bytes, dec_bytes = wl["enc_bytes"], wl["dec_bytes"]
-    if enc_ms >= dec_ms:
-        kname, kbytes, kms = wl["knames"][0], enc_bytes, enc_ms
-    else:
-        kname, kbytes, kms = wl["knames"][1], dec_bytes, dec_ms
-    achieved = kbytes / (kms * 1e-3)
-    pmc = pmc_traffic(workload)
-    traffic = None
-    if pmc and kname in pmc.get("per_launch_bytes", {}):
-        traffic = pmc["per_launch_bytes"][kname]
-    roof = {"bound": "hbm", "kernel": kname, "achieved": round(achieved / 1e9, 1),
-            "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
-            "traffic": traffic, "algorithmic_bytes_per_launch": kbytes,
-            "avg_launch_ms": round(kms, 4),
-            "enc_ms": round(enc_ms, 4), "dec_ms": round(dec_ms, 4)}
-
-    line = {"metric": wl["metric"],
-            "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
-            "higher_is_better": True, "scaling": "strong" if cfg == 5 else "weak",
-            "vs_baseline": None, "dtype": "u32", "data": "synthetic (splitmix64)",
-            "config": dict({"workload": workload, "records_per_gpu": R,
-                            "bytes_counted": "plaintext bytes through the AEAD, encrypt + decrypt",
-                            "parallelism": "records sharded per GPU, no collective"},
-                           **wl["config"]),
-            "roofline": roof}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        log("cpu baseline ...")
-        line["cpu_baseline"] = cpu_baseline()
-    if rank == 0 and args.host_inclusive and cfg == 2:
-        line["host_inclusive"] = host_inclusive(R, L)
-    if rank == 0:
-        print(json.dumps(line), flush=True)
-    if dist:
-        dist.destroy_process_group()
+def config1(orc=None):
+    """BASELINE config 1 (examples/Noise_XX_25519_ChaChaPoly_Blake2b.cpp:26-75):
+    XX loopback handshake + 1000 x 1 KiB records each way, record by record
+    (encrypt_with_ad / decrypt_with_ad), through the build's noise::
+    HandshakeState / CipherState (noise-cpp_amd/bin/config1_bench, every AEAD
+    on the GPU), beside the reference's Monocypher AEAD + handshake on one
+    host thread (oracle/_ref), in the same run."""
+    tool = os.path.join(ROOT, "noise-cpp_amd", "bin", "config1_bench")
+    if not os.path.exists(tool):
+        return {"error": "noise-cpp_amd/bin/config1_bench not built"}
+    p = subprocess.run([tool, "1000", "1024"], capture_output=True, text=True, timeout=300)
+    if p.returncode != 0:
+        return {"error": "config1_bench failed: " + p.stderr[-500:]}
+    build = json.loads(p.stdout.strip().splitlines()[-1])
+    out = {"build": build}
+    if orc is None:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+        orc = oracle_lib.Oracle()
+    if orc.ref is not None:
+        import numpy as np
+        fails = ctypes.c_int(0)
+        hs = min(orc.ref.ref_xx_bench(64, 1, ctypes.byref(fails)) / 64 for _ in range(3))
+        L, R = 1024, 1000
+        pt = np.frombuffer(orc.synthetic(R * L, SEED), dtype=np.uint8).copy()
+        ct = np.zeros(R * (L + 16), dtype=np.uint8)
+        back = np.zeros(R * L, dtype=np.uint8)
+        te = min(orc.ref.ref_batch_uniform(0, KEY, 0, pt.ctypes.data, L, ct.ctypes.data, L + 16, L, R, 1,
+                                           ctypes.byref(fails)) for _ in range(5))
+        td = min(orc.ref.ref_batch_uniform(1, KEY, 0, ct.ctypes.data, L + 16, back.ctypes.data, L, L, R,
+                                           1, ctypes.byref(fails)) for _ in range(5))
+        out["reference"] = {"handshake_ms": round(hs * 1e3, 4),
+                            "encrypt_1000_ms": round(te * 1e3, 3), "decrypt_1000_ms": round(td * 1e3, 3),
+                            "per_record_us": round((te + td) / 2 / R * 1e6, 3),
+                            "note": "monocypher.c (oracle/_ref), 1 host thread; XX handshake = both "
+                                    "parties incl. key generation (ref_xx_bench)"}
+    return out
 
 
+# ---------------------------------------------------------------- workloads
 METRIC = "GiB/s ChaChaPoly AEAD over device-resident 1 KiB Noise records, 1 & 8 GPU"
 
 
@@ -255,6 +285,38 @@ def mix64_np(z):
     z = (z ^ (z >> np.uint64(30))) * np.uint64(0xbf58476d1ce4e5b9)
     z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94d049bb133111eb)
     return z ^ (z >> np.uint64(31))
+
+
+def zipf_lengths(R):
+    """Config 4 record lengths: 64 * 2^k, P(k) ~ 1/(k+1), k = 0..10 drawn by
+    inverse CDF from splitmix64(seed 4); the top bucket clamped to 65519."""
+    import numpy as np
+    w = np.array([1.0 / (k + 1) for k in range(11)])
+    cdf = np.cumsum(w / w.sum())
+    u = mix64_np(np.uint64(4) + (np.arange(R, dtype=np.uint64) + np.uint64(1)) *
+                 np.uint64(0x9e3779b97f4a7c15)).astype(np.float64) / 2.0 ** 64
+    k = np.minimum(np.searchsorted(cdf, u, side="right"), 10)
+    return np.minimum(64 << k, 65519).astype(np.uint64)
+
+
+def tile_symbol(dec, L, contig, mode):
+    return "noise_amd::k_aead_tile<%s, %d, %s, %d, 0, 1, 256>" % (
+        "true" if dec else "false", L, "true" if contig else "false", mode)
+
+
+def make_stub_workload(args, rank, world):
+    """--stub: host-only stand-in with the real shard bookkeeping."""
+    import numpy as np
+    R, L = args.records or 1024, 64
+    n_base = rank_nonce_base(2, rank, world, R, R * world)
+    buf = np.zeros(R * L, dtype=np.uint8)
+
+    def step(evs=None):
+        np.bitwise_xor(buf, 0x5A, out=buf)
+    return {"R": R, "L": L, "n_base": n_base, "workload": "stub: %d x %d B host records per rank" % (R, L),
+            "step": step, "check": lambda: True, "metric": "stub", "config": {"record_bytes": L},
+            "pt_bytes": R * L, "enc_bytes": R * (2 * L + 16), "dec_bytes": R * (2 * L + 17),
+            "read_bytes": (R * L, R * (L + 16)), "knames": (("stub",), ("stub",))}
 
 
 def make_workload(cfg, args, rank, world, stream):
@@ -293,12 +355,15 @@ def make_workload(cfg, args, rank, world, stream):
             if evs:
                 evs[2].record(stream)
         cfgd = {"record_bytes": L, "ct_stride": L + 16, "keys": 1}
+        knames = ((tile_symbol(False, L, True, 0),), (tile_symbol(True, L, True, 0),))
+        meta = 0
     elif cfg == 3:
         # 65536 sessions x 16 records x 1 KiB, interleaved: record i belongs to
         # session s = i mod S with nonce (s << 32) + i // S; key of session s =
         # bytes [32s, 32s+32) of the splitmix64 stream with seed 0x4B4559.
         S, per, L = 65536, 16, 1024
         R = S * per
+        n_base = rank * R
         d_pt = torch.empty(R * L, dtype=torch.uint8, device="cuda")
         noise_amd.fill_synthetic(d_pt, R * L, SEED, offset=rank * R * L)
         d_keys = torch.empty(S * 32, dtype=torch.uint8, device="cuda")
@@ -323,18 +388,13 @@ def make_workload(cfg, args, rank, world, stream):
                 evs[2].record(stream)
         workload = "cfg3: 65536 sessions x 16 records x 1 KiB per GPU, interleaved, per-record key+nonce"
         metric = "GiB/s ChaChaPoly AEAD over device-resident 1 KiB Noise records, 64K sessions"
-        cfgd = {"record_bytes": L, "ct_stride": L + 16, "keys": S}
+        cfgd = {"record_bytes": L, "ct_stride": L + 16, "keys": S,
+                "session_nonces": "(s << 32) + i // 65536 (the rank is in the key, not the nonce)"}
+        knames = ((tile_symbol(False, L, True, 1),), (tile_symbol(True, L, True, 1),))
+        meta = 12 * R + 32 * S  # 4-B key index + 8-B nonce per record, key table
     elif cfg == 4:
-        # 2^20 records of 64 * 2^k bytes, P(k) ~ 1/(k+1), k = 0..10 drawn by
-        # inverse CDF from splitmix64(seed 4); the top bucket clamped to 65519
-        # (largest Noise plaintext).  Records packed at 16-byte aligned offsets.
         R = args.records or (1 << 20)
-        w = np.array([1.0 / (k + 1) for k in range(11)])
-        cdf = np.cumsum(w / w.sum())
-        u = mix64_np(np.uint64(4) + (np.arange(R, dtype=np.uint64) + np.uint64(1)) *
-                     np.uint64(0x9e3779b97f4a7c15)).astype(np.float64) / 2.0 ** 64
-        k = np.minimum(np.searchsorted(cdf, u, side="right"), 10)
-        lens = np.minimum(64 << k, 65519).astype(np.uint64)
+        lens = zipf_lengths(R)
         in_sz = (lens + np.uint64(15)) // np.uint64(16) * np.uint64(16)
         ct_sz = (lens + np.uint64(31)) // np.uint64(16) * np.uint64(16)
         in_off = np.concatenate([[0], np.cumsum(in_sz)[:-1]]).astype(np.uint64)
@@ -377,33 +437,40 @@ def make_workload(cfg, args, rank, world, stream):
             if int(d_st.sum().item()) != 0:
                 return False
             # sampled exact comparison of whole records (the padding is not a record byte)
-            idx = torch.randint(0, R, (4096,), device="cuda")
-            for r in idx.tolist()[:256]:
+            idx = torch.randint(0, R, (256,), device="cuda").tolist() + [R - 1]
+            for r in idx:
                 o, n = int(off_t[r]), int(lens_t[r])
                 if not torch.equal(d_pt[o:o + n], d_back[o:o + n]):
                     return False
             return True
-        return {"R": R, "L": L, "workload": workload, "step": step, "check": check,
+        ct_bytes = int((lens + 16).sum())
+        # the whole records call (classifier, segment / tail / small-class /
+        # generic kernels, finalize): every noise_amd kernel of the direction
+        return {"R": R, "L": L, "n_base": n_base, "workload": workload, "step": step, "check": check,
                 "metric": metric, "config": cfgd, "pt_bytes": pt_bytes,
-                "enc_bytes": pt_bytes + int((lens + 16).sum()) + 48 * R,
-                "dec_bytes": pt_bytes + int((lens + 16).sum()) + 49 * R,
-                "knames": ("k_aead_records<encrypt>", "k_aead_records<decrypt>")}
+                "enc_bytes": pt_bytes + ct_bytes + 48 * R, "dec_bytes": pt_bytes + ct_bytes + 49 * R,
+                "read_bytes": (pt_bytes + 48 * R, ct_bytes + 48 * R),
+                "knames": (("noise_amd::k_cls_", "noise_amd::k_seg_prep", "noise_amd::k_seg_tail<false",
+                            "noise_amd::k_seg_finalize<false", "noise_amd::k_aead_tile<false",
+                            "noise_amd::k_aead_records<false"),
+                           ("noise_amd::k_cls_", "noise_amd::k_seg_prep", "noise_amd::k_seg_tail<true",
+                            "noise_amd::k_seg_finalize<true", "noise_amd::k_seg_fixup",
+                            "noise_amd::k_aead_tile<true", "noise_amd::k_aead_records<true")),
+                "call_level": True}
     else:
         raise SystemExit("unknown config %d" % cfg)
 
     def check():
         return int(d_st.sum().item()) == 0 and torch.equal(d_pt, d_back)
-    return {"R": R, "L": L, "workload": workload, "step": step, "check": check,
+    return {"R": R, "L": L, "n_base": n_base, "workload": workload, "step": step, "check": check,
             "metric": metric, "config": cfgd, "pt_bytes": R * L,
-            # cfg 3 also reads a 4-B key index + 8-B nonce per record and the key table
-            "enc_bytes": R * (2 * L + 16) + ((12 * R + 32 * 65536) if cfg == 3 else 0),
-            "dec_bytes": R * (2 * L + 17) + ((12 * R + 32 * 65536) if cfg == 3 else 0),
-            "knames": ("k_aead_sessions<encrypt>", "k_aead_sessions<decrypt>") if cfg == 3 else
-                      ("k_aead_uniform<encrypt>", "k_aead_uniform<decrypt>")}
+            "enc_bytes": R * (2 * L + 16) + meta, "dec_bytes": R * (2 * L + 17) + meta,
+            "read_bytes": (R * L + meta, R * (L + 16) + meta), "knames": knames}
 
 
 def host_inclusive(R, L):
-    """Pinned host buffers -> chunked H2D || kernel || D2H pipeline (3 streams)."""
+    """Pinned host buffers -> chunked H2D || kernel || D2H pipeline (3 streams),
+    the whole call timed (persistent per-device pipeline context)."""
     import torch
     lib = noise_amd.load()
     pt = torch.empty(R * L, dtype=torch.uint8).pin_memory()
@@ -415,19 +482,216 @@ def host_inclusive(R, L):
     back = torch.empty(R * L, dtype=torch.uint8).pin_memory()
     st = torch.empty(R, dtype=torch.uint8).pin_memory()
     te, td = ctypes.c_double(), ctypes.c_double()
-    for _ in range(2):
+    best_e = best_d = 1e9
+    for _ in range(3):
+        t0 = time.perf_counter()
         assert lib.noise_gpu_encrypt_uniform_host(KEY, 0, ctypes.c_void_p(pt.data_ptr()), L,
                                                   ctypes.c_void_p(ct.data_ptr()), L + 16, L, R,
                                                   ctypes.byref(te)) == 0
+        t1 = time.perf_counter()
         assert lib.noise_gpu_decrypt_uniform_host(KEY, 0, ctypes.c_void_p(ct.data_ptr()), L + 16,
                                                   ctypes.c_void_p(back.data_ptr()), L, L,
                                                   ctypes.c_void_p(st.data_ptr()), R,
                                                   ctypes.byref(td)) == 0
+        t2 = time.perf_counter()
+        best_e, best_d = min(best_e, t1 - t0), min(best_d, t2 - t1)
     assert torch.equal(pt, back) and int(st.sum()) == 0
-    return {"encrypt_GiBps": round(R * L / te.value / GIB, 2),
-            "decrypt_GiBps": round(R * L / td.value / GIB, 2),
-            "note": "pinned host -> device -> host, 32 MiB chunks over 3 HIP streams"}
+    return {"encrypt_GiBps": round(R * L / best_e / GIB, 2),
+            "decrypt_GiBps": round(R * L / best_d / GIB, 2),
+            "note": "whole call (python wall clock), pinned host -> device -> host, 32 MiB chunks "
+                    "over 3 HIP streams, best of 3"}
+
+
+# ---------------------------------------------------------------- main
+def parse(argv):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--min-warmup-s", type=float, default=0.3,
+                    help="keep running untimed warmup steps until this much wall time has passed "
+                         "(the GPU clock ramps over ~0.1 s; see DESIGN.md)")
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5])
+    ap.add_argument("--records", type=int, default=0, help="override records per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-config1", action="store_true",
+                    help="skip the config-1 (XX loopback + 1000 x 1 KiB) leg of the N=1 line")
+    ap.add_argument("--host-inclusive", action="store_true",
+                    help="also time the pinned-host H2D->kernel->D2H pipeline (DESIGN.md)")
+    ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.config == 1:
+        print(json.dumps(dict({"metric": "config 1: XX loopback + 1000 x 1 KiB each way, per record",
+                               "config": {"workload": "cfg1"}}, **config1())), flush=True)
+        return 0
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch(args, argv)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("note: WORLD_SIZE=%d, --gpus %d; n_gpus reports the world size" % (world, args.gpus))
+    dist = None
+    if args.stub:
+        import torch
+        dev = "cpu"
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+
+        def sync():
+            pass
+        stream = None
+        wl = make_stub_workload(args, rank, world)
+    else:
+        import torch
+        torch.cuda.set_device(local)
+        dev = "cuda"
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        noise_amd.load()
+        stream = torch.cuda.current_stream()
+        sync = torch.cuda.synchronize
+        wl = make_workload(args.config, args, rank, world, stream)
+    cfg = args.config
+    R, L, workload, step = wl["R"], wl["L"], wl["workload"], wl["step"]
+
+    log("rank %d/%d: %d records x %d B, nonces [%d, %d), warmup %d" %
+        (rank, world, R, L, wl["n_base"], wl["n_base"] + R, args.warmup))
+    # correctness of the step about to be timed: all tags verify, round trip
+    # exact (checked before the warmup so no host-side idle gap -- during which
+    # the GPU clock drops -- separates the warmup from the timed steps)
+    step()
+    sync()
+    if not wl["check"]():
+        raise SystemExit("round trip failed on rank %d" % rank)
+    evs = None
+    if not args.stub:
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    tw = time.perf_counter()
+    for _ in range(args.warmup):
+        step()
+    sync()
+    while time.perf_counter() - tw < args.min_warmup_s:
+        for _ in range(4):
+            step()
+        sync()
+
+    if dist:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i] if evs else None)
+    sync()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    shards = [{"rank": rank, "nonce_lo": wl["n_base"], "nonce_hi": wl["n_base"] + R, "records": R}]
+    if dist:
+        elapsed, total_rec = reduce_over_ranks(dist, elapsed, R, dev)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, shards[0])
+        shards = gathered
+    else:
+        total_rec = R
+    bad = check_shards(shards) if cfg != 3 else None
+    if bad:
+        raise SystemExit("shard table: " + bad)
+    # the timed work was correct too
+    if not wl["check"]():
+        raise SystemExit("timed round trip failed on rank %d" % rank)
+    if evs:
+        enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+        dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+    else:
+        enc_ms = dec_ms = elapsed * 1e3 / args.steps / 2
+    log("enc %.3f ms, dec %.3f ms per launch; step %.3f ms" %
+        (enc_ms, dec_ms, elapsed * 1e3 / args.steps))
+
+    # plaintext through the AEAD (enc + dec), scaled from this rank's records
+    total_bytes = 2.0 * wl["pt_bytes"] * (total_rec / R) * args.steps
+    value = total_bytes / elapsed / GIB
+
+    line = {"metric": wl["metric"],
+            "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+            "higher_is_better": True, "scaling": "strong" if cfg == 5 else "weak",
+            "vs_baseline": None, "dtype": "u32", "data": "synthetic (splitmix64)",
+            "config": dict({"workload": workload, "records_per_gpu": R,
+                            "bytes_counted": "plaintext bytes through the AEAD, encrypt + decrypt",
+                            "parallelism": "records sharded per GPU, no collective"},
+                           **wl["config"]),
+            "roofline": roofline(cfg, wl, enc_ms, dec_ms),
+            "shards": shards}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.stub:
+        log("cpu baseline ...")
+        line["cpu_baseline"] = cpu_baseline()
+    if rank == 0 and world == 1 and cfg == 2 and not args.no_config1 and not args.stub:
+        log("config 1 leg ...")
+        line["config1"] = config1()
+    if rank == 0 and args.host_inclusive and cfg == 2 and not args.stub:
+        line["host_inclusive"] = host_inclusive(R, L)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+    return 0
+
+
+def roofline(cfg, wl, enc_ms, dec_ms):
+    """Roofline of the dominant kernel: algorithmic bytes per launch / its
+    average duration from the HIP events on its own stream (cfg 4: the whole
+    records call).  HBM traffic and VALU instruction counts come from the
+    committed rocprofv3 PMC summary of the same workload."""
+    if enc_ms >= dec_ms:
+        d, kbytes, rbytes, kms = 0, wl["enc_bytes"], wl["read_bytes"][0], enc_ms
+    else:
+        d, kbytes, rbytes, kms = 1, wl["dec_bytes"], wl["read_bytes"][1], dec_ms
+    names = wl["knames"][d]
+    achieved = kbytes / (kms * 1e-3)
+    prof = latest_profile(cfg)
+    pmc = pmc_kernels(prof, names)
+    traffic = None
+    if pmc and "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
+        # gfx950: FETCH_SIZE reports half of a wide coalesced read stream
+        traffic = int((2.0 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024)
+    roof = {"bound": "hbm", "kernel": names[0] if len(names) == 1 else
+            "records call: " + ", ".join(n.replace("noise_amd::", "") + "*" for n in names),
+            "direction": "decrypt" if d else "encrypt",
+            "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic,
+            "hbm_frac_rw": round(achieved / HBM_PEAK, 4),
+            "hbm_frac_read": round(rbytes / (kms * 1e-3) / HBM_PEAK, 4),
+            "hbm_frac_note": "rw = (bytes read + written) / t / 8 TB/s (north_star target 0.70); read = "
+                             "bytes read / t / 8 TB/s (a 1:1 read/write stream cannot exceed ~0.5)",
+            "algorithmic_bytes_per_launch": kbytes, "read_bytes_per_launch": rbytes,
+            "avg_launch_ms": round(kms, 4), "enc_ms": round(enc_ms, 4), "dec_ms": round(dec_ms, 4),
+            "pmc_source": prof[0] if prof else None,
+            "binding_roof": "valu"}
+    if pmc and "SQ_INSTS_VALU" in pmc:
+        vi = pmc["SQ_INSTS_VALU"]
+        valu = {"insts_per_launch": int(vi), "achieved": round(vi / (kms * 1e-3) / 1e9, 2),
+                "peak": round(VALU_PEAK / 1e9, 1), "unit": "G wave-instr/s",
+                "frac": round(vi / (kms * 1e-3) / VALU_PEAK, 4),
+                "issue_model": "1024 SIMDs x 2.4 GHz / 4 cycles per wave64 instruction (measured cost "
+                               "of every instruction in a ChaCha/Poly1305 stream on gfx950)"}
+        if "SQ_WAVES" in pmc and pmc["SQ_WAVES"]:
+            valu["insts_per_wave"] = int(vi / pmc["SQ_WAVES"])
+        if pmc.get("GRBM_GUI_ACTIVE"):
+            # effective clock of the profiled dispatch (GRBM_GUI_ACTIVE sums 8 XCDs)
+            busy = pmc["GRBM_GUI_ACTIVE"] / 8.0
+            valu["issue_util_profiled"] = round(vi * 4.0 / 1024.0 / busy, 4)
+        roof["valu"] = valu
+    return roof
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -411,9 +411,12 @@ __device__ __forceinline__ void poly_ad(Poly1305 &p, const uint8_t *ad,
 // --------------------------------------------------------- record walk
 // One AEAD record (Noise ENCRYPT / DECRYPT, noise.cpp:202-281 semantics).
 //   DECRYPT=false: in = plaintext[len]  -> out = ct[len] || tag[16]
-//   DECRYPT=true : in = ct[len]||tag    -> out = plaintext[len] if the tag
-//                  verifies; returns false on mismatch, and then restores
-//                  (in-place) or zeroes (out-of-place) the output.
+//   DECRYPT=true : in = ct[len]||tag    -> the tag is checked over the
+//                  ciphertext FIRST (crypto_aead_read, monocypher.c:2912-
+//                  2929); only a verified record is decrypted into out.  A
+//                  failed one leaves out untouched when in place and zeroes
+//                  it when out of place; returns false.  No unauthenticated
+//                  plaintext is ever written.
 // VEC: in/out are 16-byte aligned and len % 16 == 0 (dwordx4 path).
 template <bool DECRYPT, bool VEC>
 __device__ __forceinline__ bool aead_record(const uint32_t k[8], uint64_t n,
@@ -428,8 +431,35 @@ __device__ __forceinline__ bool aead_record(const uint32_t k[8], uint64_t n,
     poly_init(p, otk);
   }
   if (ad_len) poly_ad(p, ad, ad_len);
-
   const uint32_t nfull = len >> 6;
+  const uint32_t rem = len & 63u;
+
+  if (DECRYPT) {
+    // pass 1: MAC over the ciphertext (reads only)
+    for (uint32_t off = 0; off < len; off += 16u) {
+      const int nb = (len - off) >= 16u ? 16 : (int)(len - off);
+      const uint4 v = load16<VEC>(in + off, nb);
+      poly_block(p, v.x, v.y, v.z, v.w);
+    }
+    poly_block(p, ad_len, 0u, len, 0u);
+    uint32_t tag[4];
+    poly_final(p, tag);
+    const uint4 want = load16<VEC>(in + len, 16);
+    const uint32_t diff = (want.x ^ tag[0]) | (want.y ^ tag[1]) |
+                          (want.z ^ tag[2]) | (want.w ^ tag[3]);
+    if (diff != 0u) {
+      // tag mismatch (rare): in place leaves the buffer as it was; a copy
+      // gets zeros (no stale bytes of an earlier record)
+      if (in != out)
+        for (uint32_t off = 0; off < len; off += 16u) {
+          const int nb = (len - off) >= 16u ? 16 : (int)(len - off);
+          store16<VEC>(out + off, make_uint4(0u, 0u, 0u, 0u), nb);
+        }
+      return false;
+    }
+  }
+  // (encrypt) or pass 2 (verified decrypt): keystream XOR, encrypt MACs the
+  // ciphertext as it goes
   for (uint32_t c = 0; c < nfull; ++c) {
     uint32_t ks[16];
     chacha20_block(k, 1u + c, n_lo, n_hi, ks);
@@ -443,12 +473,10 @@ __device__ __forceinline__ bool aead_record(const uint32_t k[8], uint64_t n,
       o.y = v.y ^ ks[4 * q + 1];
       o.z = v.z ^ ks[4 * q + 2];
       o.w = v.w ^ ks[4 * q + 3];
-      if (DECRYPT) poly_block(p, v.x, v.y, v.z, v.w);
-      else poly_block(p, o.x, o.y, o.z, o.w);
+      if (!DECRYPT) poly_block(p, o.x, o.y, o.z, o.w);
       store16<VEC>(dst + 16 * q, o, 16);
     }
   }
-  const uint32_t rem = len & 63u;
   if (rem) {
     uint32_t ks[16];
     chacha20_block(k, 1u + nfull, n_lo, n_hi, ks);
@@ -461,53 +489,20 @@ __device__ __forceinline__ bool aead_record(const uint32_t k[8], uint64_t n,
       const int nb = m >= 16 ? 16 : m;
       const uint4 v = load16<VEC>(src + 16 * q, nb);
       // keystream bytes past the record end must not reach the MAC: mask
-      const uint32_t m0 = nb >= 4 ? ~0u : (nb > 0 ? (1u << (8 * nb)) - 1u : 0u);
-      const uint32_t m1 = nb >= 8 ? ~0u : (nb > 4 ? (1u << (8 * (nb - 4))) - 1u : 0u);
-      const uint32_t m2 = nb >= 12 ? ~0u : (nb > 8 ? (1u << (8 * (nb - 8))) - 1u : 0u);
-      const uint32_t m3 = nb >= 16 ? ~0u : (nb > 12 ? (1u << (8 * (nb - 12))) - 1u : 0u);
-      uint4 o;
-      o.x = (v.x ^ ks[4 * q + 0]) & m0;
-      o.y = (v.y ^ ks[4 * q + 1]) & m1;
-      o.z = (v.z ^ ks[4 * q + 2]) & m2;
-      o.w = (v.w ^ ks[4 * q + 3]) & m3;
-      if (DECRYPT) poly_block(p, v.x, v.y, v.z, v.w);
-      else poly_block(p, o.x, o.y, o.z, o.w);
+      const uint4 o = mask_bytes(make_uint4(v.x ^ ks[4 * q + 0], v.y ^ ks[4 * q + 1],
+                                            v.z ^ ks[4 * q + 2], v.w ^ ks[4 * q + 3]), nb);
+      if (!DECRYPT) poly_block(p, o.x, o.y, o.z, o.w);
       store16<VEC>(dst + 16 * q, o, nb);
     }
   }
-  // length block LE64(ad_len) || LE64(len)
-  poly_block(p, ad_len, 0u, len, 0u);
-  uint32_t tag[4];
-  poly_final(p, tag);
   if (!DECRYPT) {
+    // length block LE64(ad_len) || LE64(len)
+    poly_block(p, ad_len, 0u, len, 0u);
+    uint32_t tag[4];
+    poly_final(p, tag);
     store16<VEC>(out + len, make_uint4(tag[0], tag[1], tag[2], tag[3]), 16);
-    return true;
   }
-  const uint4 want = load16<VEC>(in + len, 16);
-  const uint32_t diff = (want.x ^ tag[0]) | (want.y ^ tag[1]) |
-                        (want.z ^ tag[2]) | (want.w ^ tag[3]);
-  if (diff == 0u) return true;
-  // Tag mismatch (rare, divergent).  In place: XOR the keystream back so
-  // the ciphertext is exactly as it was.  Out of place: zero the output.
-  const bool in_place = (in == out);
-  for (uint32_t off = 0; off < len; off += 64u) {
-    uint32_t ks[16];
-    if (in_place) chacha20_block(k, 1u + (off >> 6), n_lo, n_hi, ks);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int m = (int)(len - off) - 16 * q;
-      if (m <= 0) break;
-      const int nb = m >= 16 ? 16 : m;
-      uint4 o = make_uint4(0u, 0u, 0u, 0u);
-      if (in_place) {
-        const uint4 v = load16<VEC>(out + off + 16 * q, nb);
-        o = make_uint4(v.x ^ ks[4 * q + 0], v.y ^ ks[4 * q + 1],
-                       v.z ^ ks[4 * q + 2], v.w ^ ks[4 * q + 3]);
-      }
-      store16<VEC>(out + off + 16 * q, o, nb);
-    }
-  }
-  return false;
+  return true;
 }
 
 }  // namespace noise_amd

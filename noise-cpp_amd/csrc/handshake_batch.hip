@@ -255,9 +255,16 @@ int noise_gpu_hs_write_message(noise_gpu_hs *hs, const noise_gpu_span *payload,
   if (!hs->started) return api_arg_fail("noise_gpu_hs_start first");
   if (hs->msg >= hs->prog.msgs.size()) return api_arg_fail("handshake already finished");
   if (!my_turn(hs)) return api_arg_fail("not this party's turn to write");
-  if (payload && payload->len_all > 65535) return api_arg_fail("payload exceeds 65535 bytes");
   const hipStream_t st = (hipStream_t)stream;
   const uint64_t n = hs->n;
+  // the whole message (token bytes + payload + tag) must fit 65535 bytes, as
+  // the host HandshakeState throws length_error (noise.cpp:886): uniform
+  // lengths are refused here, per-session lengths fail their sessions with
+  // BAD_LEN on the device before any byte is written
+  const uint32_t need = overhead(hs);
+  if (payload && !payload->len && (uint64_t)payload->len_all + need > 65535)
+    return api_arg_fail("message (payload + overhead) exceeds 65535 bytes");
+  if (payload && payload->len) HS_TRY(launch_hs_check_len(hs->S, n, payload->len, need, need, st));
   HsSpan m = span_of(msg);
   m.len = nullptr;
   for (PatternToken t : hs->prog.msgs[hs->msg]) {
@@ -322,7 +329,7 @@ int noise_gpu_hs_read_message(noise_gpu_hs *hs, const noise_gpu_span *msg,
   const uint64_t n = hs->n;
   const uint32_t need = overhead(hs);
   if (msg->len) {
-    HS_TRY(launch_hs_check_len(hs->S, n, msg->len, need, st));
+    HS_TRY(launch_hs_check_len(hs->S, n, msg->len, need, 0, st));
   } else if (msg->len_all < need || msg->len_all > 65535) {
     return api_arg_fail("message length outside [overhead, 65535]");
   }

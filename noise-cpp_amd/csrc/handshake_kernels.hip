@@ -203,10 +203,14 @@ __global__ __launch_bounds__(64) void k_hs_psk(HsSession *S, uint64_t n, const u
 
 // Message length check before a read: cursor_min <= len_i <= 65535, else the
 // session fails with NOISE_GPU_HS_BAD_LEN.
+// message length len[i] + add outside [min_len, 65535]: the session fails
+// (read: len = message lengths, add 0; write: len = payload lengths, add =
+// the message's fixed bytes, so no oversized message is ever written)
 __global__ __launch_bounds__(64) void k_hs_check_len(HsSession *S, uint64_t n, const uint32_t *len,
-                                                     uint32_t min_len) {
+                                                     uint32_t min_len, uint32_t add) {
   NOISE_HS_ROW();
-  if (len[i] < min_len || len[i] > 65535u) fail(row, NOISE_GPU_HS_BAD_LEN);
+  const uint64_t m = (uint64_t)len[i] + add;
+  if (m < min_len || m > 65535u) fail(row, NOISE_GPU_HS_BAD_LEN);
 }
 
 // EncryptAndHash(src) -> dst: ct = ENCRYPT(k, nonce, h, pt) if has_k else pt;
@@ -363,8 +367,8 @@ hipError_t launch_hs_psk(HsSession *S, uint64_t n, const uint8_t *psks, uint32_t
   return hipGetLastError();
 }
 hipError_t launch_hs_check_len(HsSession *S, uint64_t n, const uint32_t *len, uint32_t min_len,
-                               hipStream_t st) {
-  hipLaunchKernelGGL(k_hs_check_len, grid_of(n), dim3(64), 0, st, S, n, len, min_len);
+                               uint32_t add, hipStream_t st) {
+  hipLaunchKernelGGL(k_hs_check_len, grid_of(n), dim3(64), 0, st, S, n, len, min_len, add);
   return hipGetLastError();
 }
 hipError_t launch_hs_encrypt_hash(HsSession *S, uint64_t n, bool has_k, uint64_t nonce,

@@ -76,7 +76,7 @@ hipError_t launch_hs_dh(HsSession *S, uint64_t n, int sk, int pk, hipStream_t st
 hipError_t launch_hs_psk(HsSession *S, uint64_t n, const uint8_t *psks, uint32_t npsk,
                          uint32_t idx, hipStream_t st);
 hipError_t launch_hs_check_len(HsSession *S, uint64_t n, const uint32_t *len, uint32_t min_len,
-                               hipStream_t st);
+                               uint32_t add, hipStream_t st);
 hipError_t launch_hs_encrypt_hash(HsSession *S, uint64_t n, bool has_k, uint64_t nonce,
                                   int src_key, const HsSpan &src, const HsSpan &dst,
                                   uint32_t *out_len, hipStream_t st);

@@ -54,6 +54,14 @@ int check_device() {
 
 void key_words(const uint8_t *key, uint32_t w[8]) { std::memcpy(w, key, 32); }
 
+// An all-zero key is "no key" (Noise HasKey() false; CipherState never
+// calls the engine then): refused rather than used as a public key.
+bool key_absent(const uint8_t *key) {
+  uint8_t acc = 0;
+  for (int i = 0; i < 32; ++i) acc |= key[i];
+  return acc == 0;
+}
+
 int arg_fail(const char *msg) {
   g_last_error = msg;
   return NOISE_GPU_E_ARG;
@@ -159,6 +167,7 @@ int noise_gpu_encrypt_uniform(const uint8_t h_key[32], uint64_t nonce0,
   int rc = check_uniform(false, d_in, in_stride, d_out, out_stride, len, d_ad,
                          ad_len, nullptr, nrec);
   if (rc || nrec == 0) return rc;
+  if (key_absent(h_key)) return arg_fail("all-zero key (no key)");
   if ((rc = check_device())) return rc;
   uint32_t k[8];
   key_words(h_key, k);
@@ -179,6 +188,7 @@ int noise_gpu_decrypt_uniform(const uint8_t h_key[32], uint64_t nonce0,
   int rc = check_uniform(true, d_in, in_stride, d_out, out_stride, len, d_ad,
                          ad_len, d_status, nrec);
   if (rc || nrec == 0) return rc;
+  if (key_absent(h_key)) return arg_fail("all-zero key (no key)");
   if ((rc = check_device())) return rc;
   uint32_t k[8];
   key_words(h_key, k);
@@ -311,6 +321,7 @@ int noise_gpu_encrypt_host(const uint8_t h_key[32], uint64_t nonce,
                            size_t len) {
   if (!h_key || !h_buf || (ad_len && !h_ad))
     return arg_fail("null key / buffer / ad");
+  if (key_absent(h_key)) return arg_fail("all-zero key (no key)");
   if (len > 0xffffffffull - 16 || ad_len > 0xffffffffull)
     return arg_fail("record too large");
   int rc = check_device();
@@ -338,6 +349,7 @@ int noise_gpu_decrypt_host(const uint8_t h_key[32], uint64_t nonce,
                            size_t ct_len) {
   if (!h_key || !h_buf || (ad_len && !h_ad))
     return arg_fail("null key / buffer / ad");
+  if (key_absent(h_key)) return arg_fail("all-zero key (no key)");
   if (ct_len < 16) {  // reference UB (noise.cpp:257); defined as bad MAC
     g_last_error = "ciphertext shorter than the tag";
     return NOISE_GPU_E_MAC;
@@ -403,9 +415,10 @@ static int records_host(bool decrypt, const uint8_t *h_keys, uint32_t nkeys,
     const noise_gpu_record &r = h_recs[i];
     const uint64_t in_len = decrypt ? (uint64_t)r.len + 16 : r.len;
     const uint64_t out_len = decrypt ? r.len : (uint64_t)r.len + 16;
-    if (r.key_idx >= nkeys || r.in_off + in_len > in_bytes ||
-        r.out_off + out_len > out_bytes ||
-        (r.ad_len && r.ad_off + r.ad_len > ad_bytes))
+    // overflow-safe: an offset near 2^64 must not wrap past the check
+    if (r.key_idx >= nkeys || in_len > in_bytes || r.in_off > in_bytes - in_len ||
+        out_len > out_bytes || r.out_off > out_bytes - out_len ||
+        (r.ad_len && (r.ad_len > ad_bytes || r.ad_off > ad_bytes - r.ad_len)))
       return arg_fail("record descriptor out of range");
   }
   int rc = check_device();
@@ -462,6 +475,7 @@ static int uniform_host(bool decrypt, const uint8_t h_key[32], uint64_t nonce0,
                         uint64_t out_stride, uint32_t len, uint8_t *h_status,
                         uint64_t nrec, double *seconds) {
   if (!h_key) return arg_fail("null key");
+  if (key_absent(h_key)) return arg_fail("all-zero key (no key)");
   int rc = check_uniform(decrypt, h_in, in_stride, h_out, out_stride, len,
                          nullptr, 0, decrypt ? (const void *)h_status : h_in,
                          nrec);

@@ -64,10 +64,21 @@ constexpr uint64_t kSegCapMax = NOISE_SEG_CAP;  // 16 Mi segments = 16 GiB per c
 #define NOISE_GRID_CAP 8192u
 #endif
 
-__device__ __forceinline__ int record_class(const noise_gpu_record &d,
+// an all-zero key row is "no key" (Noise HasKey() false, e.g. the rows
+// noise_gpu_hs_split leaves for failed handshakes): never used to encrypt
+__device__ __forceinline__ bool key_row_zero(const uint8_t *keys, uint32_t ki) {
+  const uint4 *kp = reinterpret_cast<const uint4 *>(keys + 32ull * ki);
+  const uint4 a = kp[0], b = kp[1];
+  return (a.x | a.y | a.z | a.w | b.x | b.y | b.z | b.w) == 0u;
+}
+
+// records the tile / segment kernels cannot take go to the generic class,
+// which also reports bad key rows (index out of range or all zero)
+__device__ __forceinline__ int record_class(const noise_gpu_record &d, const uint8_t *keys,
                                             uint32_t nkeys, const uint8_t *in,
                                             const uint8_t *out) {
   if (d.key_idx >= nkeys || d.ad_len != 0 || d.len == 0) return kClsGeneric;
+  if (key_row_zero(keys, d.key_idx)) return kClsGeneric;
   if (((reinterpret_cast<uintptr_t>(in + d.in_off) |
         reinterpret_cast<uintptr_t>(out + d.out_off)) & 15u) != 0)
     return kClsGeneric;
@@ -135,7 +146,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 // records, their SegRec header fields and the segment list.
 __global__ __launch_bounds__(64) void k_cls_count(
     const noise_gpu_record *__restrict__ recs, uint64_t nrec, uint32_t chunk,
-    uint32_t nkeys, const uint8_t *in, const uint8_t *out, uint32_t *part) {
+    const uint8_t *keys, uint32_t nkeys, const uint8_t *in, const uint8_t *out, uint32_t *part) {
   const uint32_t lane = threadIdx.x;
   const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
   const uint64_t e0 = b0 + chunk < nrec ? b0 + chunk : nrec;
@@ -148,7 +159,7 @@ __global__ __launch_bounds__(64) void k_cls_count(
     bool tail = false;
     if (i < e0) {
       const noise_gpu_record d = recs[i];
-      cls = record_class(d, nkeys, in, out);
+      cls = record_class(d, keys, nkeys, in, out);
       nf = cls == kClsLong ? d.len >> 10 : 0u;
       tail = cls == kClsLong && (d.len & 1023u) != 0;
     }
@@ -205,7 +216,7 @@ __global__ __launch_bounds__(64) void k_cls_scan(const uint32_t *part, uint32_t 
 
 __global__ __launch_bounds__(64) void k_cls_scatter(
     const noise_gpu_record *__restrict__ recs, uint64_t nrec, uint32_t chunk,
-    uint32_t nkeys, const uint8_t *in, const uint8_t *out,
+    const uint8_t *keys, uint32_t nkeys, const uint8_t *in, const uint8_t *out,
     const unsigned long long *wbase, RecHdr *hdr, uint32_t *idx, SegRec *rt,
     SegEntry *segs, uint32_t *tails, uint32_t *fin, uint64_t segcap) {
   const uint32_t lane = threadIdx.x;
@@ -247,7 +258,7 @@ __global__ __launch_bounds__(64) void k_cls_scatter(
     noise_gpu_record d{};
     if (i < e0) {
       d = recs[i];
-      cls = record_class(d, nkeys, in, out);
+      cls = record_class(d, keys, nkeys, in, out);
     }
     const uint32_t nf = cls == kClsLong ? d.len >> 10 : 0u;
     const bool tail = cls == kClsLong && (d.len & 1023u) != 0;
@@ -615,9 +626,13 @@ __global__ __launch_bounds__(kGenBlock) void k_aead_records(
       if (DECRYPT) status[di] = NOISE_GPU_REC_BAD_KEY;
       continue;
     }
-    const uint4 *kp = reinterpret_cast<const uint4 *>(keys + 32u * r.key_idx);
+    const uint4 *kp = reinterpret_cast<const uint4 *>(keys + 32ull * r.key_idx);
     const uint4 ka = kp[0], kb = kp[1];
     const uint32_t k[8] = {ka.x, ka.y, ka.z, ka.w, kb.x, kb.y, kb.z, kb.w};
+    if ((ka.x | ka.y | ka.z | ka.w | kb.x | kb.y | kb.z | kb.w) == 0u) {  // no key
+      if (DECRYPT) status[di] = NOISE_GPU_REC_BAD_KEY;
+      continue;
+    }
     const uint8_t *src = in + r.in_off;
     uint8_t *dst = out + r.out_off;
     const bool vec = ((reinterpret_cast<uintptr_t>(src) |
@@ -813,9 +828,9 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   SegPartial *partial = reinterpret_cast<SegPartial *>(base + o_part2);
 
   const dim3 b64(64);
-  hipLaunchKernelGGL(k_cls_count, dim3((unsigned)nw), b64, 0, stream, recs, nrec, (uint32_t)chunk, nkeys, in, out, part);
+  hipLaunchKernelGGL(k_cls_count, dim3((unsigned)nw), b64, 0, stream, recs, nrec, (uint32_t)chunk, keys, nkeys, in, out, part);
   hipLaunchKernelGGL(k_cls_scan, dim3(kCols), b64, 0, stream, part, (uint32_t)nw, wbase, hdr, segcap);
-  hipLaunchKernelGGL(k_cls_scatter, dim3((unsigned)nw), b64, 0, stream, recs, nrec, (uint32_t)chunk, nkeys, in, out, wbase, hdr, idx, rt, segs, tails, fin, segcap);
+  hipLaunchKernelGGL(k_cls_scatter, dim3((unsigned)nw), b64, 0, stream, recs, nrec, (uint32_t)chunk, keys, nkeys, in, out, wbase, hdr, idx, rt, segs, tails, fin, segcap);
 
   TileArgs ta{};
   ta.in = in;

@@ -374,6 +374,8 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
       const u32x4 ka = __builtin_nontemporal_load(kp), kb = __builtin_nontemporal_load(kp + 1);
       own_k[0] = ka.x; own_k[1] = ka.y; own_k[2] = ka.z; own_k[3] = ka.w;
       own_k[4] = kb.x; own_k[5] = kb.y; own_k[6] = kb.z; own_k[7] = kb.w;
+      // an all-zero row is "no key" (failed handshake split): not processed
+      own_bad = own_bad || (ka.x | ka.y | ka.z | ka.w | kb.x | kb.y | kb.z | kb.w) == 0u;
       own_nlo = (uint32_t)n;
       own_nhi = (uint32_t)(n >> 32);
     } else {

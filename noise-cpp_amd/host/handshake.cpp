@@ -202,8 +202,9 @@ void HandshakeState::finish_if_done() {
 
 void HandshakeState::write_message(std::vector<std::uint8_t> &payload,
                                    std::vector<std::uint8_t> &message_buffer) {
-  if (completed) throw std::logic_error("handshake already finished");
-  if (!my_turn) throw std::logic_error("not this party's turn to write");
+  if (completed) throw std::runtime_error("Handshake has already been completed!");  // noise.cpp:879-881
+  if (!my_turn)  // noise.cpp:882-885
+    throw std::runtime_error("Expected a read message call, but write message was called instead!");
   if (payload.size() > 65535) throw std::length_error("payload exceeds 65535 bytes");
   const std::size_t start = message_buffer.size();
   for (PatternToken t : message_patterns.front()) {
@@ -253,8 +254,9 @@ void HandshakeState::write_message(std::vector<std::uint8_t> &message_buffer) {
 
 void HandshakeState::read_message(std::vector<std::uint8_t> &message,
                                   std::vector<std::uint8_t> &payload_buffer) {
-  if (completed) throw std::logic_error("handshake already finished");
-  if (my_turn) throw std::logic_error("not this party's turn to read");
+  if (completed) throw std::runtime_error("Handshake has already been completed!");  // noise.cpp:975-977
+  if (my_turn)  // noise.cpp:978-981
+    throw std::runtime_error("Expected a write message call, but read message was called instead!");
   if (message.size() > 65535) throw std::length_error("message exceeds 65535 bytes");
   std::size_t off = 0;
   auto take = [&](std::size_t n) {

@@ -146,6 +146,9 @@ Pipeline::Pipeline(Direction d, const Options &o) : dir_(d), opt_(o) {
     hip_check(hipStreamCreateWithFlags(&sl->st, hipStreamNonBlocking), "slot stream");
     hip_check(hipEventCreateWithFlags(&sl->done, hipEventDisableTiming), "slot event");
   }
+  hipEvent_t ke = nullptr;
+  hip_check(hipEventCreateWithFlags(&ke, hipEventDisableTiming), "key event");
+  keys_evt_ = ke;
 }
 
 Pipeline::~Pipeline() {
@@ -170,6 +173,7 @@ Pipeline::~Pipeline() {
     if (sl->done) (void)hipEventDestroy(sl->done);
     delete sl;
   }
+  if (keys_evt_) (void)hipEventDestroy(static_cast<hipEvent_t>(keys_evt_));
 }
 
 void Pipeline::sync_all() {
@@ -247,9 +251,17 @@ std::uint64_t Pipeline::flush() {
   if (sl.nrec == 0) return 0;
   const bool dec = dir_ == Direction::Decrypt;
   const std::size_t nkeys = nonces_.size();
+  // Key rows reach the device table on the stream of the slot that first
+  // needs them.  Every slot stream waits on keys_evt_ before its kernels, and
+  // each upload waits on the previous one before recording keys_evt_ again,
+  // so the event's latest record covers every row uploaded so far, whichever
+  // slot stream carried it.
+  if (keys_uploaded_) hip_check(hipStreamWaitEvent(sl.st, static_cast<hipEvent_t>(keys_evt_), 0), "key wait");
   if (key_dirty_ < nkeys) {  // new sessions' keys (rows never change once written)
     hip_check(hipMemcpyAsync(d_keys_ + 32 * key_dirty_, h_keys_ + 32 * key_dirty_,
                              32 * (nkeys - key_dirty_), hipMemcpyHostToDevice, sl.st), "key upload");
+    hip_check(hipEventRecord(static_cast<hipEvent_t>(keys_evt_), sl.st), "key event");
+    keys_uploaded_ = true;
     key_dirty_ = nkeys;
   }
   hip_check(hipMemcpyAsync(sl.d, sl.h, sl.nrec * sizeof(noise_gpu_record), hipMemcpyHostToDevice, sl.st),

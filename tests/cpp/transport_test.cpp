@@ -6,6 +6,10 @@
 //       noise::transport::Pipeline (small slots: many flushes in flight,
 //       full-slot retries, ticket reuse), ciphertexts vs the oracle and vs
 //       the Batcher's, decrypt round trip with tampered records
+//   transport_test keyrace <sessions>   Pipeline key-table ordering: slot A
+//       uploads a large table of new sessions' keys, slot B (another stream,
+//       no upload of its own) is flushed right after with messages of the
+//       last sessions; B's ciphertexts must match the oracle
 //   transport_test bench <batcher|pipeline> <sessions> <messages> <len>
 //       host-resident throughput, encrypt then decrypt, GiB/s of plaintext
 // Sessions get random keys and start nonces; messages (0..2000 bytes, some
@@ -152,6 +156,45 @@ static int run_pipeline(int S, int M, std::uint64_t seed) {
   return fails ? 1 : 0;
 }
 
+static int run_keyrace(int S) {
+  int fails = 0;
+  std::mt19937_64 rng(99);
+  nt::Pipeline::Options o;
+  o.depth = 2;
+  o.slot_bytes = 4 << 20;
+  o.slot_records = 4096;
+  nt::Pipeline enc(nt::Pipeline::Direction::Encrypt, o);
+  std::vector<std::array<std::uint8_t, 32>> keys(S);
+  for (int s = 0; s < S; ++s) {
+    for (auto &b : keys[s]) b = (std::uint8_t)rng();
+    noise::CipherState cs;
+    cs.initialize_key(keys[s]);
+    enc.add_session(cs);
+  }
+  bytes pt(1024);
+  for (auto &b : pt) b = (std::uint8_t)rng();
+  // slot A: one message of session 0 -> uploads all S key rows on A's stream
+  enc.submit(0, pt.data(), pt.size());
+  const std::uint64_t ta = enc.flush();
+  // slot B, flushed at once: messages of the sessions uploaded last
+  const int M = 2048;
+  for (int i = 0; i < M; ++i)
+    if (!enc.submit(S - 1 - i, pt.data(), pt.size()) && fails++ < 10) std::printf("FAIL submit %d\n", i);
+  const std::uint64_t tb = enc.flush();
+  const nt::Pipeline::Batch b = enc.wait(tb);
+  if (b.size() != (std::size_t)M && fails++ < 10) std::printf("FAIL batch size %zu\n", b.size());
+  bytes want(1024 + 16);
+  for (int i = 0; i < M; ++i) {
+    const int s = S - 1 - i;
+    oracle_noise_encrypt(keys[s].data(), 0, nullptr, 0, pt.data(), pt.size(), want.data());
+    if (b.length(i) != want.size() || std::memcmp(b.data(i), want.data(), want.size()) != 0)
+      if (fails++ < 10) std::printf("FAIL keyrace record %d (session %d)\n", i, s);
+  }
+  (void)ta;
+  std::printf("keyrace sessions %d messages %d: %s (%d failures)\n", S, M, fails ? "FAIL" : "ok", fails);
+  return fails ? 1 : 0;
+}
+
 // Host-resident throughput: M messages of len bytes from one source buffer
 // (the "socket reads"), encrypt then decrypt, results checksummed (touched).
 static int run_bench(const std::string &mode, int S, long M, std::size_t len) {
@@ -239,6 +282,7 @@ static int run_bench(const std::string &mode, int S, long M, std::size_t len) {
 int main(int argc, char **argv) {
   if (argc > 1 && std::string(argv[1]) == "pipeline")
     return run_pipeline(std::atoi(argv[2]), std::atoi(argv[3]), std::strtoull(argv[4], nullptr, 0));
+  if (argc > 1 && std::string(argv[1]) == "keyrace") return run_keyrace(std::atoi(argv[2]));
   if (argc > 1 && std::string(argv[1]) == "bench")
     return run_bench(argv[2], std::atoi(argv[3]), std::atol(argv[4]), std::strtoul(argv[5], nullptr, 0));
   const int S = argc > 1 ? std::atoi(argv[1]) : 100;

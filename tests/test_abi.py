@@ -40,7 +40,7 @@ def test_status_strings():
 
 def test_argument_validation_precedes_device():
     lib = noise_amd.load()
-    key = bytes(32)
+    key = bytes(range(1, 33))
     buf = ctypes.c_void_p(0x10000)
     # null buffers
     assert lib.noise_gpu_encrypt_uniform(key, 0, None, 64, buf, 80, 64, None, 0, 0, 4, None) == noise_amd.E_ARG
@@ -57,6 +57,30 @@ def test_argument_validation_precedes_device():
                                          None, 4, None) == noise_amd.E_ARG
     # empty batches are no-ops, even without a device
     assert lib.noise_gpu_encrypt_uniform(key, 0, None, 0, None, 0, 0, None, 0, 0, 0, None) == noise_amd.OK
+    # an all-zero key is "no key" (Noise HasKey() false): refused, never used
+    zero = bytes(32)
+    assert lib.noise_gpu_encrypt_uniform(zero, 0, buf, 64, ctypes.c_void_p(0x90000), 80, 64, None, 0, 0, 4,
+                                         None) == noise_amd.E_ARG
+    assert lib.noise_gpu_decrypt_uniform(zero, 0, buf, 80, ctypes.c_void_p(0x90000), 64, 64, None, 0, 0,
+                                         buf, 4, None) == noise_amd.E_ARG
+    hbuf = ctypes.create_string_buffer(64)
+    assert lib.noise_gpu_encrypt_host(zero, 0, None, 0, hbuf, 16) == noise_amd.E_ARG
+    assert lib.noise_gpu_decrypt_host(zero, 0, None, 0, hbuf, 32) == noise_amd.E_ARG
+    # descriptor offsets near 2^64 must not wrap past the host bounds check
+    rec = noise_amd.Record(in_off=(1 << 64) - 8, out_off=0, nonce=0, ad_off=0, len=64, ad_len=0,
+                           key_idx=0, reserved=0)
+    out = ctypes.create_string_buffer(256)
+    src = ctypes.create_string_buffer(256)
+    assert lib.noise_gpu_encrypt_records_host(key, 1, ctypes.byref(rec), 1, src, 256, out, 256,
+                                              None, 0) == noise_amd.E_ARG
+    rec = noise_amd.Record(in_off=0, out_off=(1 << 64) - 16, nonce=0, ad_off=0, len=64, ad_len=0,
+                           key_idx=0, reserved=0)
+    assert lib.noise_gpu_encrypt_records_host(key, 1, ctypes.byref(rec), 1, src, 256, out, 256,
+                                              None, 0) == noise_amd.E_ARG
+    rec = noise_amd.Record(in_off=0, out_off=0, nonce=0, ad_off=(1 << 64) - 4, len=64, ad_len=8,
+                           key_idx=0, reserved=0)
+    assert lib.noise_gpu_encrypt_records_host(key, 1, ctypes.byref(rec), 1, src, 256, out, 256,
+                                              src, 16) == noise_amd.E_ARG
 
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a GPU is visible")

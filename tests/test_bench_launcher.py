@@ -1,0 +1,63 @@
+"""CPU: the real `python bench.py --gpus N` launcher (no WORLD_SIZE in the
+environment) spawns N ranks, each rank gets its own nonce range, the ranks
+meet over gloo for the barrier / max-over-ranks / shard table, and exactly one
+JSON line comes out with n_gpus = N.  The workload is the --stub host
+stand-in (no GPU here); the launcher, the rank environment and the reductions
+are the ones the GPU run uses."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+
+
+def run_bench(*extra, gpus=2, timeout=240):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--stub", "--gpus", str(gpus),
+                        "--steps", "3", "--warmup", "1", "--min-warmup-s", "0", *extra],
+                       capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
+    return p
+
+
+@pytest.mark.parametrize("gpus", [2, 3])
+def test_launcher_spawns_ranks_one_json_line(gpus):
+    p = run_bench("--records", "100", gpus=gpus)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == gpus and d["steps"] == 3 and d["scaling"] == "weak"
+    shards = sorted(d["shards"], key=lambda s: s["rank"])
+    assert [s["rank"] for s in shards] == list(range(gpus))
+    # disjoint nonce ranges, one per rank, each of the rank's own records
+    assert [(s["nonce_lo"], s["nonce_hi"]) for s in shards] == \
+        [(100 * r, 100 * (r + 1)) for r in range(gpus)]
+    # every rank logged itself
+    for r in range(gpus):
+        assert "rank %d/%d" % (r, gpus) in p.stderr
+    # value counts every rank's records
+    assert d["value"] > 0 and d["config"]["records_per_gpu"] == 100
+
+
+def test_single_gpu_path_does_not_launch():
+    p = run_bench("--records", "64", gpus=1)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["n_gpus"] == 1 and len(d["shards"]) == 1
+
+
+def test_check_shards_flags_overlap():
+    sys.path.insert(0, ROOT)
+    import bench
+    ok = [{"rank": 0, "nonce_lo": 0, "nonce_hi": 10}, {"rank": 1, "nonce_lo": 10, "nonce_hi": 20}]
+    assert bench.check_shards(ok) is None
+    bad = [{"rank": 0, "nonce_lo": 0, "nonce_hi": 11}, {"rank": 1, "nonce_lo": 10, "nonce_hi": 20}]
+    assert "share" in bench.check_shards(bad)
+    # strong scaling (cfg 5): contiguous slices of one range cover it exactly
+    spans = [bench.shard(8 << 20, r, 8) for r in range(8)]
+    assert spans[0][0] == 0 and spans[-1][1] == 8 << 20
+    assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))

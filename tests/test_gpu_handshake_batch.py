@@ -170,6 +170,44 @@ def test_batch_message_length_checks():
     R.close()
 
 
+def test_batch_write_payload_length_checks():
+    """write_message: a message (token bytes + payload + tag) must fit 65535
+    bytes (noise.cpp:886).  A uniform payload length that does not is refused
+    on the host; per-session lengths fail exactly their sessions with
+    HS_BAD_LEN on the device before any byte of them is written."""
+    n = 64
+    E = noise_amd.NoiseGpuError
+    I = noise_amd.HandshakeBatch("NN", True, n)
+    I.start()
+    ov = I.info().overhead  # "e" = 32 bytes, no key yet: no tag
+    assert ov == 32
+    stride = 65536 + 64
+    buf = torch.full((n * stride,), 0xAB, dtype=torch.uint8, device="cuda")
+    pay = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+    with pytest.raises(E):  # uniform: 65535 - 32 + 1 bytes of payload
+        I.write_message(noise_amd.span(buf, stride=stride), noise_amd.span(pay, stride=stride,
+                                                                           length=65535 - ov + 1))
+    plen = torch.full((n,), 10, dtype=torch.int32, device="cuda")
+    plen[3], plen[40] = 65535 - ov + 1, 0x7fffffff
+    plen[41] = 65535 - ov  # the largest payload that fits
+    mlen = torch.zeros(n, dtype=torch.int32, device="cuda")
+    I.write_message(noise_amd.span(buf, stride=stride),
+                    noise_amd.span(pay, stride=stride, lens=plen), d_msg_len=mlen)
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    I.status(st)
+    torch.cuda.synchronize()
+    s, m = st.cpu().numpy(), mlen.cpu().numpy()
+    for i in range(n):
+        if i in (3, 40):
+            assert s[i] == noise_amd.HS_BAD_LEN, i
+            row = buf[i * stride:(i + 1) * stride]
+            assert bool((row == 0xAB).all()), ("failed session's message was written", i)
+        else:
+            assert s[i] == 0, i
+            assert m[i] == ov + (65535 - ov if i == 41 else 10), i
+    I.close()
+
+
 def test_batch_api_rules_and_shared_static_key():
     """Host-side rules of the batched API (turn order, keys before start, psk
     count, finished/split order) and a stride-0 static key (one server key for

@@ -409,6 +409,17 @@ def test_transport_pipeline(sessions, messages, seed):
     assert "ok (0 failures)" in r.stdout
 
 
+def test_transport_pipeline_key_upload_order():
+    """Pipeline key table: slot A uploads 2^18 new sessions'
+    key rows (8 MiB) on its stream; slot B, flushed immediately on another
+    stream with no upload of its own, encrypts messages of the last sessions.
+    B's stream must wait for A's upload: ciphertexts equal the oracle's."""
+    exe = os.path.join(noise_amd.ROOT, "noise-cpp_amd", "bin", "transport_test")
+    r = subprocess.run([exe, "keyrace", str(1 << 18)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "ok (0 failures)" in r.stdout
+
+
 def _sessions_case(rng, nkeys, per, length):
     keys = [rng.randbytes(32) for _ in range(nkeys)]
     nrec = nkeys * per
@@ -480,3 +491,33 @@ def test_sessions_bad_key_index(oracle):
                                length, d_st, nrec)
     st = host(d_st)
     assert st[5] == noise_amd.REC_BAD_KEY and sum(st) == noise_amd.REC_BAD_KEY
+
+
+def test_sessions_zero_key_row_refused(oracle):
+    """An all-zero key row (Noise HasKey() false; what noise_gpu_hs_split
+    leaves for a failed handshake) is never used to encrypt: the sessions
+    kernel skips the record (nothing written) and decrypt reports BAD_KEY."""
+    rng = random.Random(78)
+    nkeys, per, length = 64, 2, 1024
+    keys, s, nonces, pt, nrec = _sessions_case(rng, nkeys, per, length)
+    keys = list(keys)
+    keys[int(s[9])] = bytes(32)
+    zero_recs = [r for r in range(nrec) if s[r] == s[9]]
+    d_keys = dev(b"".join(keys))
+    d_out = torch.full((nrec * (length + 16),), 0xEE, dtype=torch.uint8, device="cuda")
+    noise_amd.encrypt_sessions(d_keys, nkeys, dev(s.view(np.uint8)), dev(nonces.view(np.uint8)), dev(pt),
+                               length, d_out, length + 16, length, nrec)
+    out = host(d_out)
+    for r in range(nrec):
+        blk = out[r * 1040:(r + 1) * 1040]
+        if r in zero_recs:
+            assert blk == b"\xee" * 1040, r
+        else:
+            assert blk == oracle.encrypt(keys[s[r]], int(nonces[r]), b"", pt[r * 1024:(r + 1) * 1024].tobytes())
+    d_st = torch.full((nrec,), 9, dtype=torch.uint8, device="cuda")
+    d_back = torch.zeros(nrec * length, dtype=torch.uint8, device="cuda")
+    noise_amd.decrypt_sessions(d_keys, nkeys, dev(s.view(np.uint8)), dev(nonces.view(np.uint8)), d_out,
+                               length + 16, d_back, length, length, d_st, nrec)
+    st = host(d_st)
+    for r in range(nrec):
+        assert st[r] == (noise_amd.REC_BAD_KEY if r in zero_recs else noise_amd.REC_OK), r

@@ -248,3 +248,50 @@ def test_offsets_beyond_2gib(oracle):
     for i, (L, *_rest) in enumerate(recs):
         o = int(desc[i]["in_off"]) - gap_in
         assert back[o:o + L] == pts[i], (i, L)
+
+
+def test_mixed_batch_zero_key_rows(oracle):
+    """All-zero key rows are "no key": records of every class (tile sizes,
+    1 KiB, long segmented records, generic) under such a row are not written
+    and decrypt reports BAD_KEY; the rest of the batch is unaffected."""
+    rng = random.Random(6)
+    keys, recs = make_batch(rng, n_small=2100, n_big=30, nkeys=6)
+    keys[4] = bytes(32)
+    pts = [rng.randbytes(r[0]) for r in recs]
+    zero = {i for i, r in enumerate(recs) if r[2] == 4}
+    assert len(zero) > 100 and any(recs[i][0] >= 16385 for i in zero)
+    desc, in_bytes, out_bytes, ad_bytes = layout(recs, decrypt=False)
+    inb = bytearray(in_bytes)
+    fill(inb, desc, pts, "in_off")
+    adb = bytearray(ad_bytes)
+    fill(adb, desc, [r[1] for r in recs], "ad_off")
+    d_keys, d_ad = dev(b"".join(keys)), dev(adb)
+    d_out = torch.full((out_bytes,), 0xEE, dtype=torch.uint8, device="cuda")
+    noise_amd.encrypt_records(d_keys, len(keys), dev(desc.view(np.uint8)), len(recs), dev(inb), d_out, d_ad)
+    out = host(d_out)
+    cts = []
+    for i, (L, ad, ki, n, _, _) in enumerate(recs):
+        o = int(desc[i]["out_off"])
+        if i in zero:
+            assert out[o:o + L + 16] == b"\xee" * (L + 16), (i, L)
+            cts.append(bytearray(L + 16))
+        else:
+            want = oracle.encrypt(keys[ki], n, ad, pts[i])
+            assert out[o:o + L + 16] == want, (i, L)
+            cts.append(bytearray(want))
+    ddesc, din, dout, _ = layout(recs, decrypt=True)
+    cin = bytearray(din)
+    fill(cin, ddesc, cts, "in_off")
+    d_st = torch.full((len(recs),), 9, dtype=torch.uint8, device="cuda")
+    d_back = torch.full((dout,), 0x77, dtype=torch.uint8, device="cuda")
+    noise_amd.decrypt_records(d_keys, len(keys), dev(ddesc.view(np.uint8)), len(recs), dev(cin), d_back,
+                              d_st, d_ad)
+    st = host(d_st)
+    back = host(d_back)
+    for i, (L, *_rest) in enumerate(recs):
+        o = int(ddesc[i]["out_off"])
+        if i in zero:
+            assert st[i] == noise_amd.REC_BAD_KEY, (i, L)
+            assert back[o:o + L] == b"\x77" * L, ("nothing written", i, L)
+        else:
+            assert st[i] == noise_amd.REC_OK and back[o:o + L] == pts[i], (i, L)

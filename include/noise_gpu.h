@@ -130,6 +130,13 @@ int noise_gpu_decrypt_records(const uint8_t *d_keys, uint32_t nkeys,
                               const uint8_t *d_ad, uint8_t *d_status,
                               void *stream);
 
+/* The descriptor path keeps a grow-only device scratch per (device,
+ * stream) that holds, between the kernels of a call, copies of the long
+ * records' keys, their one-time Poly1305 keys and partial sums.  This zeroes
+ * it (stream-ordered after the calls already issued on `stream`), e.g. at
+ * session teardown.  The host-buffer entry points below wipe it themselves. */
+int noise_gpu_scratch_wipe(void *stream);
+
 /* ---- device-resident many-session batches (BASELINE config 3) ---------
  * nrec records of `len` plaintext bytes, record i under key row
  * d_keys[d_key_idx[i]] (a [nkeys][32] table, 16-byte aligned) with Noise

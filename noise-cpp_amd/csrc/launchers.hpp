@@ -22,6 +22,9 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
                                const uint8_t *ad, uint8_t *status,
                                hipStream_t stream);
 
+// zero the records-path scratch of (current device, stream)
+hipError_t records_scratch_wipe(hipStream_t stream);
+
 bool sessions_supported(uint32_t len, const void *in, uint64_t in_stride,
                         const void *out, uint64_t out_stride);
 
@@ -34,6 +37,28 @@ hipError_t launch_aead_sessions(bool decrypt, const uint8_t *keys,
                                 hipStream_t stream);
 
 hipError_t launch_rekey(uint8_t *keys, uint64_t nkeys, hipStream_t stream);
+
+// ---- latency path (single_kernels.hip): one record per launch, staged in
+// host-mapped pinned memory that the kernel reads and writes directly.
+constexpr uint32_t kOneMaxAd = 8192;  // larger AD takes the copy-staged path
+struct OneLayout {
+  uint64_t ad, in, tag, out, total;
+};
+// [0,64) header (u32 done word, u32 status) | AD | record | tag | output
+__host__ __device__ inline OneLayout one_layout(uint32_t ad_len, uint32_t len) {
+  const uint64_t a16 = (ad_len + 15ull) & ~15ull, l16 = (len + 15ull) & ~15ull;
+  OneLayout o;
+  o.ad = 64;
+  o.in = o.ad + a16;
+  o.tag = o.in + l16;
+  o.out = o.tag + 16;
+  o.total = o.out + l16 + 16;
+  return o;
+}
+size_t one_lds_bytes(uint32_t ad_len, uint32_t len);
+hipError_t launch_aead_one(bool decrypt, const uint32_t key[8], uint64_t nonce,
+                           uint8_t *d_base, uint32_t len, uint32_t ad_len, uint32_t seq,
+                           hipStream_t stream);
 
 hipError_t launch_x25519(const uint8_t *scalars, const uint8_t *points,
                          uint8_t *out, uint64_t n, hipStream_t stream);

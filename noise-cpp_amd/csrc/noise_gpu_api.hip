@@ -98,6 +98,13 @@ struct Staging {
     if (h) (void)hipHostFree(h);
     if (stream) (void)hipStreamDestroy(stream);
   }
+  // hygiene after a call: the pinned image and the device scratch
+  // (hipMemsetAsync on the staging stream; a later call's copies queue after it)
+  void wipe(size_t bytes) {
+    if (bytes > cap) bytes = cap;
+    if (h) std::memset(h, 0, bytes);
+    if (d && stream) (void)hipMemsetAsync(d, 0, bytes, stream);
+  }
   int reserve(size_t bytes) {
     int cur = 0;
     HIP_TRY(hipGetDevice(&cur));
@@ -120,6 +127,104 @@ struct Staging {
   }
 };
 thread_local Staging g_stage;
+
+// Per-thread latency-path context (single_kernels.hip): a stream and a
+// host-mapped, coherent pinned staging image the kernel reads and writes
+// over PCIe; completion is a done word the kernel stores last.
+struct OneCtx {
+  int dev = -1;
+  hipStream_t stream = nullptr;
+  uint8_t *h = nullptr;  // host view
+  uint8_t *d = nullptr;  // device view of the same memory
+  size_t cap = 0;
+  uint32_t seq = 0;
+  ~OneCtx() {
+    if (h) {
+      std::memset(h, 0, cap);
+      (void)hipHostFree(h);
+    }
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+  int reserve(size_t bytes) {
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    if (cur != dev) {
+      if (stream) (void)hipStreamDestroy(stream);
+      stream = nullptr;
+      dev = cur;
+      HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    }
+    if (bytes <= cap) return NOISE_GPU_OK;
+    size_t want = cap ? cap : 16384;
+    while (want < bytes) want *= 2;
+    if (h) {
+      std::memset(h, 0, cap);
+      (void)hipHostFree(h);
+    }
+    h = d = nullptr;
+    cap = 0;
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h), want,
+                          hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(h, 0, want);
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&d), h, 0));
+    cap = want;
+    return NOISE_GPU_OK;
+  }
+  // launch already issued with `s`: wait for the done word
+  int wait(uint32_t s) {
+    volatile uint32_t *done = reinterpret_cast<volatile uint32_t *>(h);
+    for (uint64_t spin = 0;; ++spin) {
+      if (*done == s) return NOISE_GPU_OK;
+      if ((spin & 1023u) == 1023u) {  // now and then: has the stream failed or ended?
+        const hipError_t e = hipStreamQuery(stream);
+        if (e == hipSuccess) {
+          if (*done == s) return NOISE_GPU_OK;
+          g_last_error = "latency kernel ended without its done word";
+          return NOISE_GPU_E_HIP;
+        }
+        if (e != hipErrorNotReady) return hip_fail(e, "latency kernel");
+      }
+    }
+  }
+};
+thread_local OneCtx g_one;
+
+// One record through the latency kernel.  dec: in = ct (len bytes) + tag.
+// Returns the kernel's status in *st (decrypt); out receives len (+16 on
+// encrypt) bytes.  Staging is wiped after use.
+int one_record(bool dec, const uint8_t key[32], uint64_t nonce, const uint8_t *ad, uint32_t ad_len,
+               const uint8_t *in, uint32_t len, const uint8_t *tag, uint8_t *out, uint32_t *st) {
+  const noise_amd::OneLayout lay = noise_amd::one_layout(ad_len, len);
+  int rc = g_one.reserve(lay.total);
+  if (rc) return rc;
+  OneCtx &c = g_one;
+  if (ad_len) std::memcpy(c.h + lay.ad, ad, ad_len);
+  if (len) std::memcpy(c.h + lay.in, in, len);
+  if (dec) std::memcpy(c.h + lay.tag, tag, 16);
+  uint32_t s = ++c.seq;
+  if (s == 0) s = c.seq = 1;
+  uint32_t k[8];
+  key_words(key, k);
+  const hipError_t e = noise_amd::launch_aead_one(dec, k, nonce, c.d, len, ad_len, s, c.stream);
+  std::memset(k, 0, sizeof k);
+  if (e != hipSuccess) {
+    std::memset(c.h + 64, 0, lay.total - 64);
+    return hip_fail(e, "launch_aead_one");
+  }
+  rc = c.wait(s);
+  if (rc == NOISE_GPU_OK) {
+    const uint32_t status = dec ? reinterpret_cast<volatile uint32_t *>(c.h)[1] : 0u;
+    if (st) *st = status;
+    if (!dec) {
+      std::memcpy(out, c.h + lay.out, len);
+      std::memcpy(out + len, c.h + lay.out + ((len + 15ull) & ~15ull), 16);
+    } else if (status == NOISE_GPU_REC_OK) {
+      std::memcpy(out, c.h + lay.out, len);
+    }
+  }
+  std::memset(c.h + 4, 0, lay.total - 4);  // hygiene: AD, record, output, status
+  return rc;
+}
 
 inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
@@ -302,6 +407,13 @@ int noise_gpu_x25519(const uint8_t *d_scalars, const uint8_t *d_points,
   return NOISE_GPU_OK;
 }
 
+int noise_gpu_scratch_wipe(void *stream) {
+  int rc = check_device();
+  if (rc) return rc;
+  HIP_TRY(noise_amd::records_scratch_wipe((hipStream_t)stream));
+  return NOISE_GPU_OK;
+}
+
 int noise_gpu_fill_synthetic(uint8_t *d_dst, uint64_t offset, uint64_t nbytes,
                              uint64_t seed, void *stream) {
   if (nbytes == 0) return NOISE_GPU_OK;
@@ -322,26 +434,32 @@ int noise_gpu_encrypt_host(const uint8_t h_key[32], uint64_t nonce,
   if (!h_key || !h_buf || (ad_len && !h_ad))
     return arg_fail("null key / buffer / ad");
   if (key_absent(h_key)) return arg_fail("all-zero key (no key)");
-  if (len > 0xffffffffull - 16 || ad_len > 0xffffffffull)
-    return arg_fail("record too large");
+  if (len > 0xffffffffull - 16 || ad_len > 0xffffffffull) return arg_fail("record too large");
   int rc = check_device();
   if (rc) return rc;
+  if (ad_len <= noise_amd::kOneMaxAd && len <= 65535)  // latency kernel, mapped staging
+    return one_record(false, h_key, nonce, h_ad, (uint32_t)ad_len, h_buf, (uint32_t)len, nullptr,
+                      h_buf, nullptr);
+  // large AD or record: copy-staged through device scratch, the lane walk
   const size_t ad_sz = align16(ad_len), rec_sz = align16(len + 16);
   if ((rc = g_stage.reserve(ad_sz + rec_sz))) return rc;
   Staging &s = g_stage;
   std::memcpy(s.h, h_ad, ad_len);
   std::memcpy(s.h + ad_sz, h_buf, len);
-  HIP_TRY(hipMemcpyAsync(s.d, s.h, ad_sz + len, hipMemcpyHostToDevice, s.stream));
   uint32_t k[8];
   key_words(h_key, k);
-  HIP_TRY(noise_amd::launch_aead_uniform(false, k, nonce, s.d + ad_sz, 0,
-                                         s.d + ad_sz, 0, (uint32_t)len, s.d, 0,
-                                         (uint32_t)ad_len, nullptr, 1, s.stream));
-  HIP_TRY(hipMemcpyAsync(s.h + ad_sz, s.d + ad_sz, len + 16, hipMemcpyDeviceToHost, s.stream));
-  HIP_TRY(hipStreamSynchronize(s.stream));
-  std::memcpy(h_buf, s.h + ad_sz, len + 16);
-  std::memset(s.h, 0, ad_sz + len + 16);  // plaintext/ciphertext hygiene
-  return NOISE_GPU_OK;
+  hipError_t e = hipMemcpyAsync(s.d, s.h, ad_sz + len, hipMemcpyHostToDevice, s.stream);
+  if (e == hipSuccess)
+    e = noise_amd::launch_aead_uniform(false, k, nonce, s.d + ad_sz, 0, s.d + ad_sz, 0,
+                                       (uint32_t)len, s.d, 0, (uint32_t)ad_len, nullptr, 1,
+                                       s.stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(s.h + ad_sz, s.d + ad_sz, len + 16, hipMemcpyDeviceToHost, s.stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+  if (e == hipSuccess) std::memcpy(h_buf, s.h + ad_sz, len + 16);
+  std::memset(k, 0, sizeof k);
+  s.wipe(ad_sz + rec_sz);
+  return e == hipSuccess ? NOISE_GPU_OK : hip_fail(e, "encrypt_host (staged)");
 }
 
 int noise_gpu_decrypt_host(const uint8_t h_key[32], uint64_t nonce,
@@ -354,30 +472,40 @@ int noise_gpu_decrypt_host(const uint8_t h_key[32], uint64_t nonce,
     g_last_error = "ciphertext shorter than the tag";
     return NOISE_GPU_E_MAC;
   }
-  if (ct_len > 0xffffffffull || ad_len > 0xffffffffull)
-    return arg_fail("record too large");
+  if (ct_len > 0xffffffffull || ad_len > 0xffffffffull) return arg_fail("record too large");
   int rc = check_device();
   if (rc) return rc;
   const size_t len = ct_len - 16;
-  const size_t ad_sz = align16(ad_len), in_sz = align16(ct_len),
-               out_sz = align16(len);
-  if ((rc = g_stage.reserve(ad_sz + in_sz + out_sz + 16))) return rc;
-  Staging &s = g_stage;
-  uint8_t *d_in = s.d + ad_sz, *d_out = d_in + in_sz, *d_st = d_out + out_sz;
-  std::memcpy(s.h, h_ad, ad_len);
-  std::memcpy(s.h + ad_sz, h_buf, ct_len);
-  HIP_TRY(hipMemcpyAsync(s.d, s.h, ad_sz + ct_len, hipMemcpyHostToDevice, s.stream));
-  uint32_t k[8];
-  key_words(h_key, k);
-  HIP_TRY(noise_amd::launch_aead_uniform(true, k, nonce, d_in, 0, d_out, 0,
-                                         (uint32_t)len, s.d, 0,
-                                         (uint32_t)ad_len, d_st, 1, s.stream));
-  uint8_t *h_out = s.h + ad_sz + in_sz;
-  HIP_TRY(hipMemcpyAsync(h_out, d_out, out_sz + 16, hipMemcpyDeviceToHost, s.stream));
-  HIP_TRY(hipStreamSynchronize(s.stream));
-  const uint8_t st = h_out[out_sz];
-  if (st == NOISE_GPU_REC_OK) std::memcpy(h_buf, h_out, len);
-  std::memset(s.h, 0, ad_sz + in_sz + out_sz + 16);
+  uint32_t st = NOISE_GPU_REC_BAD_MAC;
+  if (ad_len <= noise_amd::kOneMaxAd && len <= 65535) {
+    rc = one_record(true, h_key, nonce, h_ad, (uint32_t)ad_len, h_buf, (uint32_t)len,
+                    h_buf + len, h_buf, &st);
+  } else {  // large AD or record: copy-staged through device scratch, the lane walk
+    const size_t ad_sz = align16(ad_len), in_sz = align16(ct_len), out_sz = align16(len);
+    if ((rc = g_stage.reserve(ad_sz + in_sz + out_sz + 16))) return rc;
+    Staging &s = g_stage;
+    uint8_t *d_in = s.d + ad_sz, *d_out = d_in + in_sz, *d_st = d_out + out_sz;
+    std::memcpy(s.h, h_ad, ad_len);
+    std::memcpy(s.h + ad_sz, h_buf, ct_len);
+    uint32_t k[8];
+    key_words(h_key, k);
+    uint8_t *h_out = s.h + ad_sz + in_sz;
+    hipError_t e = hipMemcpyAsync(s.d, s.h, ad_sz + ct_len, hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess)
+      e = noise_amd::launch_aead_uniform(true, k, nonce, d_in, 0, d_out, 0, (uint32_t)len, s.d, 0,
+                                         (uint32_t)ad_len, d_st, 1, s.stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(h_out, d_out, out_sz + 16, hipMemcpyDeviceToHost, s.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+    std::memset(k, 0, sizeof k);
+    if (e == hipSuccess) {
+      st = h_out[out_sz];
+      if (st == NOISE_GPU_REC_OK) std::memcpy(h_buf, h_out, len);
+    }
+    s.wipe(ad_sz + in_sz + out_sz + 16);
+    rc = e == hipSuccess ? NOISE_GPU_OK : hip_fail(e, "decrypt_host (staged)");
+  }
+  if (rc) return rc;
   if (st != NOISE_GPU_REC_OK) {
     g_last_error = "Invalid MAC";
     return NOISE_GPU_E_MAC;
@@ -386,19 +514,15 @@ int noise_gpu_decrypt_host(const uint8_t h_key[32], uint64_t nonce,
 }
 
 int noise_gpu_rekey_host(uint8_t h_key[32]) {
+  // k <- ENCRYPT(k, 2^64-2, empty, 0^32)[0..32) (noise.cpp:429-439)
   if (!h_key) return arg_fail("null key");
   int rc = check_device();
   if (rc) return rc;
-  if ((rc = g_stage.reserve(32))) return rc;
-  Staging &s = g_stage;
-  std::memcpy(s.h, h_key, 32);
-  HIP_TRY(hipMemcpyAsync(s.d, s.h, 32, hipMemcpyHostToDevice, s.stream));
-  HIP_TRY(noise_amd::launch_rekey(s.d, 1, s.stream));
-  HIP_TRY(hipMemcpyAsync(s.h, s.d, 32, hipMemcpyDeviceToHost, s.stream));
-  HIP_TRY(hipStreamSynchronize(s.stream));
-  std::memcpy(h_key, s.h, 32);
-  std::memset(s.h, 0, 32);
-  return NOISE_GPU_OK;
+  uint8_t zero[32] = {0}, out[48];
+  rc = one_record(false, h_key, ~0ull - 1ull, nullptr, 0, zero, 32, nullptr, out, nullptr);
+  if (rc == NOISE_GPU_OK) std::memcpy(h_key, out, 32);
+  std::memset(out, 0, sizeof out);
+  return rc;
 }
 
 // ---- host descriptor batches (CipherState::encrypt_batch/decrypt_batch)
@@ -433,20 +557,25 @@ static int records_host(bool decrypt, const uint8_t *h_keys, uint32_t nkeys,
   std::memcpy(s.h + o_recs, h_recs, sizeof(noise_gpu_record) * nrec);
   if (in_bytes) std::memcpy(s.h + o_in, h_in, in_bytes);
   if (ad_bytes) std::memcpy(s.h + o_ad, h_ad, ad_bytes);
-  HIP_TRY(hipMemcpyAsync(s.d, s.h, o_out, hipMemcpyHostToDevice, s.stream));
-  if (ad_bytes)
-    HIP_TRY(hipMemcpyAsync(s.d + o_ad, s.h + o_ad, ad_bytes, hipMemcpyHostToDevice, s.stream));
-  HIP_TRY(noise_amd::launch_aead_records(
-      decrypt, s.d + o_keys, nkeys,
-      reinterpret_cast<const noise_gpu_record *>(s.d + o_recs), nrec, s.d + o_in,
-      s.d + o_out, s.d + o_ad, decrypt ? s.d + o_st : nullptr, s.stream));
-  HIP_TRY(hipMemcpyAsync(s.h + o_out, s.d + o_out, o_st + nrec - o_out,
-                         hipMemcpyDeviceToHost, s.stream));
-  HIP_TRY(hipStreamSynchronize(s.stream));
-  if (out_bytes) std::memcpy(h_out, s.h + o_out, out_bytes);
-  if (decrypt) std::memcpy(h_status, s.h + o_st, nrec);
-  std::memset(s.h, 0, total);
-  return NOISE_GPU_OK;
+  hipError_t e = hipMemcpyAsync(s.d, s.h, o_out, hipMemcpyHostToDevice, s.stream);
+  if (e == hipSuccess && ad_bytes)
+    e = hipMemcpyAsync(s.d + o_ad, s.h + o_ad, ad_bytes, hipMemcpyHostToDevice, s.stream);
+  if (e == hipSuccess)
+    e = noise_amd::launch_aead_records(
+        decrypt, s.d + o_keys, nkeys,
+        reinterpret_cast<const noise_gpu_record *>(s.d + o_recs), nrec, s.d + o_in,
+        s.d + o_out, s.d + o_ad, decrypt ? s.d + o_st : nullptr, s.stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(s.h + o_out, s.d + o_out, o_st + nrec - o_out, hipMemcpyDeviceToHost,
+                       s.stream);
+  if (e == hipSuccess) e = noise_amd::records_scratch_wipe(s.stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+  if (e == hipSuccess) {
+    if (out_bytes) std::memcpy(h_out, s.h + o_out, out_bytes);
+    if (decrypt) std::memcpy(h_status, s.h + o_st, nrec);
+  }
+  s.wipe(total);  // keys, plaintext, ciphertext: host image and device scratch
+  return e == hipSuccess ? NOISE_GPU_OK : hip_fail(e, "records_host");
 }
 
 int noise_gpu_encrypt_records_host(const uint8_t *h_keys, uint32_t nkeys,
@@ -470,10 +599,50 @@ int noise_gpu_decrypt_records_host(const uint8_t *h_keys, uint32_t nkeys,
 }
 
 // ---- host-resident uniform batches: chunked 3-stream pipeline ----------
+// Streams and device chunk buffers persist per (thread, device); a call
+// pays only its copies and kernels (and the wipe of the chunks it used).
+namespace {
+struct PipeCtx {
+  static constexpr int kDepth = 3;
+  static constexpr uint64_t kChunk = 32ull << 20;  // bytes in + out per chunk
+  int dev = -1;
+  hipStream_t st[kDepth] = {};
+  uint8_t *buf[kDepth] = {};  // [in | out | status] of one chunk
+  ~PipeCtx() { release(); }
+  void release() {
+    for (int i = 0; i < kDepth; ++i) {
+      if (st[i]) (void)hipStreamSynchronize(st[i]);
+      if (buf[i]) {
+        (void)hipMemset(buf[i], 0, kChunk + (kChunk >> 4));
+        (void)hipFree(buf[i]);
+      }
+      if (st[i]) (void)hipStreamDestroy(st[i]);
+      buf[i] = nullptr;
+      st[i] = nullptr;
+    }
+    dev = -1;
+  }
+  int ready() {
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    if (cur == dev) return NOISE_GPU_OK;
+    release();
+    for (int i = 0; i < kDepth; ++i) {
+      HIP_TRY(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
+      HIP_TRY(hipMalloc(&buf[i], kChunk + (kChunk >> 4)));
+    }
+    dev = cur;
+    return NOISE_GPU_OK;
+  }
+};
+thread_local PipeCtx g_pipe;
+}  // namespace
+
 static int uniform_host(bool decrypt, const uint8_t h_key[32], uint64_t nonce0,
                         const uint8_t *h_in, uint64_t in_stride, uint8_t *h_out,
                         uint64_t out_stride, uint32_t len, uint8_t *h_status,
                         uint64_t nrec, double *seconds) {
+  const auto t0 = std::chrono::steady_clock::now();  // the whole call is timed
   if (!h_key) return arg_fail("null key");
   if (key_absent(h_key)) return arg_fail("all-zero key (no key)");
   int rc = check_uniform(decrypt, h_in, in_stride, h_out, out_stride, len,
@@ -486,55 +655,45 @@ static int uniform_host(bool decrypt, const uint8_t h_key[32], uint64_t nonce0,
     return NOISE_GPU_OK;
   }
   if ((rc = check_device())) return rc;
+  if ((rc = g_pipe.ready())) return rc;
+  PipeCtx &P = g_pipe;
   const uint64_t in_rec = decrypt ? (uint64_t)len + 16 : len;
   const uint64_t out_rec = decrypt ? len : (uint64_t)len + 16;
-  // device chunks are packed (stride = record size); ~32 MiB per chunk
-  const uint64_t per = std::max<uint64_t>(1, (32ull << 20) / (in_rec + out_rec + 1));
-  constexpr int kDepth = 3;
-  hipStream_t st[kDepth] = {};
-  uint8_t *d_in[kDepth] = {}, *d_out[kDepth] = {}, *d_stat[kDepth] = {};
+  // device chunks are packed (stride = record size), ~32 MiB of in + out
+  const uint64_t per = std::max<uint64_t>(1, PipeCtx::kChunk / (in_rec + out_rec + 1));
+  if (per * (in_rec + out_rec) + per > PipeCtx::kChunk + (PipeCtx::kChunk >> 4))
+    return arg_fail("record too large for the host pipeline");
   uint32_t k[8];
   key_words(h_key, k);
-  auto cleanup = [&]() {
-    for (int i = 0; i < kDepth; ++i) {
-      if (st[i]) (void)hipStreamSynchronize(st[i]);
-      if (d_in[i]) (void)hipFree(d_in[i]);
-      if (d_out[i]) (void)hipFree(d_out[i]);
-      if (d_stat[i]) (void)hipFree(d_stat[i]);
-      if (st[i]) (void)hipStreamDestroy(st[i]);
-    }
-  };
   hipError_t e = hipSuccess;
-  for (int i = 0; i < kDepth && e == hipSuccess; ++i) {
-    e = hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipMalloc(&d_in[i], per * in_rec);
-    if (e == hipSuccess) e = hipMalloc(&d_out[i], per * out_rec);
-    if (e == hipSuccess && decrypt) e = hipMalloc(&d_stat[i], per);
-  }
-  if (e != hipSuccess) {
-    cleanup();
-    return hip_fail(e, "pipeline setup");
-  }
-  const auto t0 = std::chrono::steady_clock::now();
+  uint64_t used[PipeCtx::kDepth] = {0, 0, 0};
   for (uint64_t first = 0, c = 0; first < nrec && e == hipSuccess; first += per, ++c) {
     const uint64_t n = std::min(per, nrec - first);
-    const int b = (int)(c % kDepth);
-    e = hipMemcpy2DAsync(d_in[b], in_rec, h_in + first * in_stride, in_stride,
-                         in_rec, n, hipMemcpyHostToDevice, st[b]);
+    const int b = (int)(c % PipeCtx::kDepth);
+    uint8_t *d_in = P.buf[b], *d_out = d_in + per * in_rec, *d_stat = d_out + per * out_rec;
+    used[b] = std::max(used[b], per * (in_rec + out_rec) + per);
+    e = hipMemcpy2DAsync(d_in, in_rec, h_in + first * in_stride, in_stride,
+                         in_rec, n, hipMemcpyHostToDevice, P.st[b]);
     if (e == hipSuccess)
-      e = noise_amd::launch_aead_uniform(decrypt, k, nonce0 + first, d_in[b],
-                                         in_rec, d_out[b], out_rec, len,
-                                         nullptr, 0, 0, d_stat[b], n, st[b]);
+      e = noise_amd::launch_aead_uniform(decrypt, k, nonce0 + first, d_in,
+                                         in_rec, d_out, out_rec, len,
+                                         nullptr, 0, 0, decrypt ? d_stat : nullptr, n, P.st[b]);
     if (e == hipSuccess)
-      e = hipMemcpy2DAsync(h_out + first * out_stride, out_stride, d_out[b],
-                           out_rec, out_rec, n, hipMemcpyDeviceToHost, st[b]);
+      e = hipMemcpy2DAsync(h_out + first * out_stride, out_stride, d_out,
+                           out_rec, out_rec, n, hipMemcpyDeviceToHost, P.st[b]);
     if (e == hipSuccess && decrypt)
-      e = hipMemcpyAsync(h_status + first, d_stat[b], n, hipMemcpyDeviceToHost, st[b]);
+      e = hipMemcpyAsync(h_status + first, d_stat, n, hipMemcpyDeviceToHost, P.st[b]);
   }
-  for (int i = 0; i < kDepth && e == hipSuccess; ++i) e = hipStreamSynchronize(st[i]);
+  std::memset(k, 0, sizeof k);
+  for (int i = 0; i < PipeCtx::kDepth && e == hipSuccess; ++i) e = hipStreamSynchronize(P.st[i]);
   const auto t1 = std::chrono::steady_clock::now();
-  cleanup();
-  if (e != hipSuccess) return hip_fail(e, "host pipeline");
+  // hygiene: the chunks held plaintext and ciphertext
+  for (int i = 0; i < PipeCtx::kDepth; ++i)
+    if (used[i]) (void)hipMemsetAsync(P.buf[i], 0, used[i], P.st[i]);
+  if (e != hipSuccess) {
+    g_pipe.release();
+    return hip_fail(e, "host pipeline");
+  }
   if (seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
   return NOISE_GPU_OK;
 }

@@ -650,15 +650,29 @@ __global__ __launch_bounds__(kGenBlock) void k_aead_records(
 // Calls on one stream are ordered, so they may share the buffer; a buffer
 // only grows (hipFree waits for the device, so a smaller one still in use by
 // an earlier launch is never released under it).
+struct ScratchEntry {
+  int dev;
+  hipStream_t stream;
+  void *ptr;
+  size_t size;
+};
+static std::mutex g_scratch_mu;
+static std::vector<ScratchEntry> g_scratch;
+
+static void scratch_find(int dev, hipStream_t stream, void **p, size_t *size) {
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  for (const ScratchEntry &en : g_scratch)
+    if (en.dev == dev && en.stream == stream) {
+      *p = en.ptr;
+      *size = en.size;
+      return;
+    }
+}
+
 static hipError_t scratch_get(void **p, size_t bytes, hipStream_t stream) {
-  struct Entry {
-    int dev;
-    hipStream_t stream;
-    void *ptr;
-    size_t size;
-  };
-  static std::mutex mu;
-  static std::vector<Entry> cache;
+  using Entry = ScratchEntry;
+  auto &mu = g_scratch_mu;
+  auto &cache = g_scratch;
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
@@ -680,6 +694,20 @@ static hipError_t scratch_get(void **p, size_t bytes, hipStream_t stream) {
   cache.push_back({dev, stream, ptr, bytes});
   *p = ptr;
   return hipSuccess;
+}
+
+// Zero the scratch of (current device, stream): the long-record table holds
+// key copies, one-time Poly1305 keys and partial sums between the kernels of
+// a call.  Stream-ordered after the call's kernels.
+hipError_t records_scratch_wipe(hipStream_t stream) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  void *ptr = nullptr;
+  size_t size = 0;
+  scratch_find(dev, stream, &ptr, &size);
+  if (!ptr) return hipSuccess;
+  return hipMemsetAsync(ptr, 0, size, stream);
 }
 
 static inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }

@@ -56,6 +56,24 @@ def test_records_path_emulated(emu_bin, mode, nrec, seed, gap):
     assert "ok (0 failures)" in r.stdout
 
 
+def test_host_entry_points_emulated_and_wiped():
+    """The C ABI's host-buffer entry points (noise_gpu_api.hip: the latency
+    kernel for single records, the staged lane walk for AD > 8 KiB, rekey, the
+    records path with its scratch, the uniform host pipeline) on the CPU under
+    AddressSanitizer, bit-exact against the oracle, and after EVERY call every
+    buffer the engine allocated is zero: no key, plaintext, ciphertext or
+    one-time key is left in staging or scratch (monocypher.c:163-167)."""
+    r = subprocess.run(["make", "-C", EMU, "GRID_CAP=3u", "api"], capture_output=True, text=True,
+                       timeout=900)
+    if r.returncode != 0:
+        pytest.fail("emulation build failed:\n" + r.stdout[-2000:] + r.stderr[-4000:])
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
+    r = subprocess.run([os.path.join(EMU, "build", "emu_api")], capture_output=True, text=True,
+                       timeout=900, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]
+    assert "emu_api ok" in r.stdout
+
+
 def test_records_segment_overflow_emulated(emu_bin_small_cap):
     # long records past the 300-segment scratch fall back to the generic kernel
     r = _run(emu_bin_small_cap, "cfg4", 700, 7, 0)

@@ -96,6 +96,30 @@ def test_golden_single_record_host_path(golden):
         assert noise_amd.decrypt_host(r["key"], r["nonce"], r["ad"], r["ct"]) == r["pt"]
 
 
+@pytest.mark.parametrize("ad_len", [0, 64, 100, 9000])
+def test_single_record_host_lengths(oracle, ad_len):
+    """CipherState's per-record path (noise_gpu_encrypt_host / _decrypt_host:
+    the latency kernel for AD <= 8 KiB and records <= 65535 B, the staged lane
+    walk otherwise) at every record-size regime up to the Noise maximum and
+    beyond, vs the oracle; a tampered record fails and is left untouched."""
+    rng = random.Random(ad_len + 1)
+    key = rng.randbytes(32)
+    for length in (0, 1, 15, 16, 17, 64, 65, 1000, 1024, 4095, 16384, 16385, 65472, 65473, 65519,
+                   65535, 70000):
+        if ad_len == 9000 and length > 20000:
+            continue
+        n = rng.getrandbits(64) % (2**64 - 2)
+        ad, pt = rng.randbytes(ad_len), rng.randbytes(length)
+        ct = noise_amd.encrypt_host(key, n, ad, pt)
+        assert ct == oracle.encrypt(key, n, ad, pt), (length, ad_len)
+        assert noise_amd.decrypt_host(key, n, ad, ct) == pt, (length, ad_len)
+        bad = bytearray(ct)
+        bad[rng.randrange(len(bad))] ^= 4
+        with pytest.raises(noise_amd.NoiseGpuError) as e:
+            noise_amd.decrypt_host(key, n, ad, bytes(bad))
+        assert e.value.code == noise_amd.E_MAC
+
+
 def test_kats_and_rekey(oracle):
     for k, n, ad, pt, ct in (oracle_lib.KAT_K1, oracle_lib.KAT_K2, oracle_lib.KAT_K3):
         assert noise_amd.encrypt_host(bytes.fromhex(k), n, bytes.fromhex(ad),

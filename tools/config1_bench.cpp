@@ -85,6 +85,9 @@ int main(int argc, char **argv) {
       auto w = make_records(16, len);
       const auto o = w;
       per_record(warm.i_send, warm.r_recv, w, o);
+      auto wb = make_records(records, len);  // the batch path's staging, once
+      warm.i_send.encrypt_batch(wb);
+      warm.r_recv.decrypt_batch(wb);
     }
     // handshake: best of 5 (each one a fresh pair of parties)
     double hs = 1e9;

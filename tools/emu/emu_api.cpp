@@ -1,0 +1,166 @@
+// emu_api.cpp -- the C ABI's host-buffer entry points (noise_gpu_api.hip)
+// with their kernels (the latency kernel single_kernels.hip, the lane walk,
+// the records path, the host pipeline) compiled as host C++ through the HIP
+// stand-in, under AddressSanitizer, against the C oracle.  After every call
+// it scans every buffer the engine allocated (tracked by the stand-in's
+// hipMalloc / hipHostMalloc) and requires it to be all zero -- no key,
+// plaintext, ciphertext or one-time key left behind in staging or scratch
+// (the reference wipes after every use: monocypher.c:163-167,
+// noise.cpp:221-223).  The one exception is the 4-byte done word at the head
+// of the latency path's mapped staging.
+//
+//   emu_api            -> "emu_api ok (N calls, M scans)" or FAIL lines
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+#include "noise_gpu.h"
+
+extern "C" {
+void oracle_noise_encrypt(const uint8_t key[32], uint64_t n, const uint8_t *ad, size_t ad_len,
+                          const uint8_t *pt, size_t len, uint8_t *out);
+int oracle_noise_decrypt(const uint8_t key[32], uint64_t n, const uint8_t *ad, size_t ad_len,
+                         const uint8_t *ct, size_t ct_len, uint8_t *out);
+void oracle_rekey(const uint8_t key[32], uint8_t out[32]);
+}
+
+static int fails = 0, scans = 0, calls = 0;
+#define CHECK(c, ...)                      \
+  do {                                     \
+    if (!(c)) {                            \
+      if (fails < 30) {                    \
+        std::printf("FAIL: " __VA_ARGS__); \
+        std::printf("\n");                 \
+      }                                    \
+      ++fails;                             \
+    }                                      \
+  } while (0)
+
+// every engine allocation zero (bytes [0,4) of host allocations: done word)
+static void scan(const char *after) {
+  ++scans;
+  std::lock_guard<std::mutex> lk(emu::alloc_mu);
+  for (const auto &[p, a] : emu::allocations()) {
+    const uint8_t *b = static_cast<const uint8_t *>(p);
+    for (size_t i = a.host ? 4 : 0; i < a.size; ++i)
+      if (b[i]) {
+        CHECK(false, "after %s: %s allocation of %zu bytes has byte %zu = %02x", after,
+              a.host ? "host" : "device", a.size, i, b[i]);
+        break;
+      }
+  }
+}
+
+int main() {
+  std::mt19937_64 rng(12345);
+  auto rbytes = [&](size_t n) {
+    std::vector<uint8_t> v(n);
+    for (auto &x : v) x = (uint8_t)rng();
+    return v;
+  };
+  uint8_t key[32];
+  for (auto &x : key) x = (uint8_t)rng();
+  // ---- single records: latency kernel (AD <= 8192) and the staged path
+  const size_t lens[] = {0, 1, 15, 16, 17, 63, 64, 65, 100, 1000, 1024, 1040, 4096, 5000, 16384,
+                         65519, 65535, 70000};
+  const size_t ads[] = {0, 7, 64, 100, 9000};
+  for (size_t L : lens)
+    for (size_t A : ads) {
+      if (L > 20000 && A == 9000) continue;
+      const uint64_t n = rng() % 1000 + (L == 16 ? (1ull << 32) - 1 : 0);
+      const auto pt = rbytes(L), ad = rbytes(A);
+      std::vector<uint8_t> want(L + 16), buf(pt);
+      buf.resize(L + 16);
+      oracle_noise_encrypt(key, n, ad.data(), A, pt.data(), L, want.data());
+      ++calls;
+      int rc = noise_gpu_encrypt_host(key, n, A ? ad.data() : nullptr, A, buf.data(), L);
+      CHECK(rc == NOISE_GPU_OK && buf == want, "encrypt_host L=%zu A=%zu rc=%d", L, A, rc);
+      scan("encrypt_host");
+      ++calls;
+      rc = noise_gpu_decrypt_host(key, n, A ? ad.data() : nullptr, A, buf.data(), L + 16);
+      CHECK(rc == NOISE_GPU_OK && std::memcmp(buf.data(), pt.data(), L) == 0,
+            "decrypt_host L=%zu A=%zu rc=%d", L, A, rc);
+      scan("decrypt_host");
+      // tampered: MAC failure, buffer untouched
+      std::vector<uint8_t> bad(want);
+      bad[rng() % bad.size()] ^= 0x20;
+      const std::vector<uint8_t> snap(bad);
+      ++calls;
+      rc = noise_gpu_decrypt_host(key, n, A ? ad.data() : nullptr, A, bad.data(), L + 16);
+      CHECK(rc == NOISE_GPU_E_MAC && bad == snap, "tampered L=%zu A=%zu rc=%d", L, A, rc);
+      scan("decrypt_host (tampered)");
+    }
+  // ---- rekey
+  for (int i = 0; i < 4; ++i) {
+    uint8_t k[32], w[32];
+    for (auto &x : k) x = (uint8_t)(i ? rng() : 0);
+    oracle_rekey(k, w);
+    ++calls;
+    const int rc = noise_gpu_rekey_host(k);
+    CHECK(rc == NOISE_GPU_OK && std::memcmp(k, w, 32) == 0, "rekey_host %d", i);
+    scan("rekey_host");
+  }
+  // ---- descriptor batch between host buffers (records path + its scratch)
+  for (int big = 0; big < 2; ++big) {
+    const uint32_t nrec = big ? 2300 : 40;  // above / below the classifier threshold
+    const uint32_t nkeys = 3;
+    const auto keys = rbytes(32 * nkeys);
+    std::vector<noise_gpu_record> recs(nrec);
+    std::vector<std::vector<uint8_t>> pts(nrec);
+    uint64_t in_b = 0, out_b = 0;
+    for (uint32_t i = 0; i < nrec; ++i) {
+      const uint32_t L = (i % 13 == 0) ? 2048 + (uint32_t)(rng() % 5000) : (uint32_t)(rng() % 700);
+      pts[i] = rbytes(L);
+      recs[i] = noise_gpu_record{in_b, out_b, rng() % 100000, 0, L, 0, (uint32_t)(rng() % nkeys), 0};
+      in_b += (L + 15) & ~15u;
+      out_b += (L + 31) & ~15u;
+    }
+    std::vector<uint8_t> hin(in_b + 1), hout(out_b + 1);
+    for (uint32_t i = 0; i < nrec; ++i)
+      if (!pts[i].empty()) std::memcpy(hin.data() + recs[i].in_off, pts[i].data(), pts[i].size());
+    ++calls;
+    int rc = noise_gpu_encrypt_records_host(keys.data(), nkeys, recs.data(), nrec, hin.data(), in_b,
+                                            hout.data(), out_b, nullptr, 0);
+    CHECK(rc == NOISE_GPU_OK, "encrypt_records_host rc=%d", rc);
+    std::vector<uint8_t> w(8192);
+    for (uint32_t i = 0; i < nrec; ++i) {
+      oracle_noise_encrypt(keys.data() + 32 * recs[i].key_idx, recs[i].nonce, nullptr, 0,
+                           pts[i].data(), pts[i].size(), w.data());
+      CHECK(std::memcmp(hout.data() + recs[i].out_off, w.data(), pts[i].size() + 16) == 0,
+            "records_host record %u (len %u)", i, recs[i].len);
+    }
+    scan(big ? "encrypt_records_host (classified)" : "encrypt_records_host (small)");
+  }
+  // ---- uniform batch between host buffers (pipeline)
+  {
+    const uint32_t L = 256, R = 300;
+    const auto pt = rbytes((size_t)L * R);
+    std::vector<uint8_t> ct((size_t)(L + 16) * R), back((size_t)L * R), st(R, 9);
+    double secs = 0;
+    ++calls;
+    int rc = noise_gpu_encrypt_uniform_host(key, 7, pt.data(), L, ct.data(), L + 16, L, R, &secs);
+    CHECK(rc == NOISE_GPU_OK, "encrypt_uniform_host rc=%d", rc);
+    std::vector<uint8_t> w(L + 16);
+    for (uint32_t i = 0; i < R; i += 37) {
+      oracle_noise_encrypt(key, 7 + i, nullptr, 0, pt.data() + (size_t)i * L, L, w.data());
+      CHECK(std::memcmp(ct.data() + (size_t)i * (L + 16), w.data(), L + 16) == 0, "uniform_host %u", i);
+    }
+    scan("encrypt_uniform_host");
+    ++calls;
+    rc = noise_gpu_decrypt_uniform_host(key, 7, ct.data(), L + 16, back.data(), L, L, st.data(), R,
+                                        &secs);
+    CHECK(rc == NOISE_GPU_OK && back == pt, "decrypt_uniform_host rc=%d", rc);
+    for (uint32_t i = 0; i < R; ++i) CHECK(st[i] == 0, "uniform_host status %u", i);
+    scan("decrypt_uniform_host");
+  }
+  if (fails) {
+    std::printf("emu_api FAIL (%d failures, %d calls, %d scans)\n", fails, calls, scans);
+    return 1;
+  }
+  std::printf("emu_api ok (%d calls, %d scans)\n", calls, scans);
+  return 0;
+}

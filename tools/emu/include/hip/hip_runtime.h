@@ -12,7 +12,10 @@
 // LDS-DMA is a synchronous 16-byte copy; s_waitcnt / fences are no-ops and
 // s_wave_barrier is a real barrier of the wave's threads.
 #pragma once
+#define NOISE_HIP_EMU 1
 #include <atomic>
+#include <map>
+#include <mutex>
 #include <barrier>
 #include <cstdint>
 #include <cstring>
@@ -68,6 +71,32 @@ struct Ctx {
 };
 inline thread_local Ctx ctx;
 inline dim3 grid_dim, block_dim;
+// the running block's barrier (__syncthreads) and dynamic LDS
+inline std::barrier<> *block_bar = nullptr;
+inline unsigned char *dyn_lds = nullptr;
+
+// every hipMalloc / hipHostMalloc allocation, for tests that inspect what
+// the engine leaves in its buffers (secret hygiene)
+struct Alloc {
+  size_t size;
+  bool host;
+};
+inline std::mutex alloc_mu;
+inline std::map<void *, Alloc> &allocations() {
+  static std::map<void *, Alloc> m;
+  return m;
+}
+inline void *track(void *p, size_t n, bool host) {
+  if (p) {
+    std::lock_guard<std::mutex> lk(alloc_mu);
+    allocations()[p] = Alloc{n, host};
+  }
+  return p;
+}
+inline void untrack(void *p) {
+  std::lock_guard<std::mutex> lk(alloc_mu);
+  allocations().erase(p);
+}
 
 template <class T>
 inline uint64_t to_bits(T v) {
@@ -105,13 +134,17 @@ inline uint64_t ballot(bool p) {
 
 // run kernel(args...) over the grid: blocks in sequence, threads in parallel
 template <class K, class... A>
-void launch(K kernel, dim3 g, dim3 b, A... args) {
+void launch_shm(K kernel, dim3 g, dim3 b, size_t shmem, A... args) {
   grid_dim = g;
   block_dim = b;
   const unsigned nt = b.x;
   const unsigned nw = (nt + 63) / 64;
   for (unsigned bx = 0; bx < g.x; ++bx) {
     std::vector<Wave> waves(nw);
+    std::barrier<> bar((std::ptrdiff_t)nt);
+    block_bar = &bar;
+    std::vector<unsigned char> lds(shmem + 16, 0xCD);  // LDS is not zeroed on a GPU either
+    dyn_lds = lds.data();
     std::vector<std::thread> th;
     th.reserve(nt);
     for (unsigned t = 0; t < nt; ++t) {
@@ -124,10 +157,22 @@ void launch(K kernel, dim3 g, dim3 b, A... args) {
       });
     }
     for (auto &x : th) x.join();
+    block_bar = nullptr;
+    dyn_lds = nullptr;
   }
+}
+template <class K, class... A>
+void launch(K kernel, dim3 g, dim3 b, A... args) {
+  launch_shm(kernel, g, b, 0, args...);
 }
 
 }  // namespace emu
+
+#define __syncthreads() (emu::block_bar->arrive_and_wait())
+#define __threadfence_system() ((void)0)
+#define __ATOMIC_RELAXED_ __ATOMIC_RELAXED
+#define __HIP_MEMORY_SCOPE_SYSTEM 0
+#define __hip_atomic_store(p, v, order, scope) __atomic_store_n((p), (v), __ATOMIC_SEQ_CST)
 
 #define threadIdx (emu::ctx.tid)
 #define blockIdx (emu::ctx.bid)
@@ -138,6 +183,12 @@ template <class T>
 inline T __shfl(T v, int src, int width = 64) {
   (void)width;
   return emu::shfl(v, src);
+}
+template <class T>
+inline T __shfl_down(T v, unsigned d, int width = 64) {
+  (void)width;
+  const int src = emu::ctx.lane + (int)d;
+  return emu::shfl(v, src < 64 ? src : emu::ctx.lane);
 }
 template <class T>
 inline T __shfl_xor(T v, int mask, int width = 64) {
@@ -179,7 +230,7 @@ inline unsigned long long atomicMin(unsigned long long *p, unsigned long long v)
 }
 
 #define hipLaunchKernelGGL(kernel, grid, block, shmem, stream, ...)              \
-  emu::launch(kernel, dim3(grid), dim3(block), __VA_ARGS__)
+  emu::launch_shm(kernel, dim3(grid), dim3(block), (size_t)(shmem), __VA_ARGS__)
 
 inline hipError_t hipGetLastError() { return hipSuccess; }
 // launches run synchronously in program order: streams and events are no-ops
@@ -197,14 +248,38 @@ inline hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
 inline hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned) { return hipSuccess; }
 inline hipError_t hipGetDevice(int *d) { *d = 0; return hipSuccess; }
 inline hipError_t hipMalloc(void **p, size_t n) {
-  *p = std::malloc(n);
+  *p = emu::track(std::calloc(n ? n : 1, 1), n, false);
   return *p ? hipSuccess : hipErrorMemoryAllocation;
+}
+#define hipHostMallocDefault 0u
+#define hipHostMallocMapped 2u
+#define hipHostMallocCoherent 0x40000000u
+inline hipError_t hipHostMalloc(void **p, size_t n, unsigned) {
+  *p = emu::track(std::calloc(n ? n : 1, 1), n, true);
+  return *p ? hipSuccess : hipErrorMemoryAllocation;
+}
+template <class T>
+inline hipError_t hipHostMalloc(T **p, size_t n, unsigned f) {
+  return hipHostMalloc(reinterpret_cast<void **>(p), n, f);
+}
+inline hipError_t hipHostFree(void *p) {
+  emu::untrack(p);
+  std::free(p);
+  return hipSuccess;
+}
+inline hipError_t hipHostGetDevicePointer(void **d, void *h, unsigned) {
+  *d = h;
+  return hipSuccess;
 }
 template <class T>
 inline hipError_t hipMalloc(T **p, size_t n) {  // HIP's typed overload
   return hipMalloc(reinterpret_cast<void **>(p), n);
 }
-inline hipError_t hipFree(void *p) { std::free(p); return hipSuccess; }
+inline hipError_t hipFree(void *p) {
+  emu::untrack(p);
+  std::free(p);
+  return hipSuccess;
+}
 enum hipMemcpyKind { hipMemcpyHostToDevice, hipMemcpyDeviceToHost, hipMemcpyDeviceToDevice };
 inline hipError_t hipMemset(void *p, int v, size_t n) {
   std::memset(p, v, n);
@@ -222,5 +297,28 @@ inline hipError_t hipDeviceSynchronize() { return hipSuccess; }
 inline const char *hipGetErrorString(hipError_t) { return "emulated HIP error"; }
 inline hipError_t hipMemsetAsync(void *p, int v, size_t n, hipStream_t) {
   std::memset(p, v, n);
+  return hipSuccess;
+}
+
+enum { hipErrorNotReady = 600 };
+inline hipError_t hipStreamQuery(hipStream_t) { return hipSuccess; }
+inline hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+inline hipError_t hipStreamDestroy(hipStream_t) { return hipSuccess; }
+inline hipError_t hipEventDestroy(hipEvent_t) { return hipSuccess; }
+inline hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
+inline hipError_t hipGetDeviceCount(int *n) { *n = 1; return hipSuccess; }
+struct hipDeviceProp_t {
+  char gcnArchName[256];
+};
+inline hipError_t hipGetDeviceProperties(hipDeviceProp_t *p, int) {
+  std::strcpy(p->gcnArchName, "gfx950:sramecc+:xnack-");
+  return hipSuccess;
+}
+enum hipFuncAttribute { hipFuncAttributeMaxDynamicSharedMemorySize = 8 };
+inline hipError_t hipFuncSetAttribute(const void *, hipFuncAttribute, int) { return hipSuccess; }
+inline hipError_t hipMemcpy2DAsync(void *d, size_t dp, const void *s, size_t sp, size_t w, size_t h,
+                                   hipMemcpyKind, hipStream_t) {
+  for (size_t r = 0; r < h; ++r)
+    std::memmove((char *)d + r * dp, (const char *)s + r * sp, w);
   return hipSuccess;
 }

@@ -11,6 +11,13 @@
 // swap is an arithmetic mask, so all 64 lanes of a wave run the same
 // instruction stream (constant time per lane, no divergence).  Inversion by
 // the standard 254-squaring / 11-multiplication chain for p-2.
+//
+// Formula source: fe_mul / fe_sq below are the public-domain ref10 schoolbook
+// products in radix 2^25.5 (SUPERCOP crypto_scalarmult/curve25519/ref10,
+// fe_mul.c / fe_sq.c), the same formulas monocypher.c:1225-1325 carries; the
+// term order and the 19*g / 2*f temporaries follow them.  The carry handling
+// (unsigned, uncarried sums fed to the next product, one carry pass per
+// product) is this file's own.
 #pragma once
 #include "chachapoly_device.hpp"
 

@@ -1,0 +1,136 @@
+"""GPU parity at BASELINE full size for configs 3, 4 and 5 (config 2:
+test_gpu_parity.py::test_config2_full_size_round_trip), built exactly as
+bench.py builds them.  Size-independent properties over the whole batch --
+every tag verifies, decrypt(encrypt(x)) == x byte for byte -- plus sampled
+records bit-exact against the CPU oracle: a random sample, every length class,
+the largest Noise records (65519 B, noise.cpp:886, 982) and the last record."""
+import os
+import random
+import sys
+
+import numpy as np
+import pytest
+
+import noise_amd
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+ROOT = noise_amd.ROOT
+sys.path.insert(0, ROOT)
+SEED = 0x4E4F495345
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    noise_amd.load()
+    torch.cuda.set_device(0)
+    yield
+    torch.cuda.empty_cache()
+
+
+def _bytes(t):
+    return t.cpu().numpy().tobytes()
+
+
+def test_config3_full_size_sessions(oracle):
+    """65536 sessions x 16 records x 1 KiB through encrypt_sessions /
+    decrypt_sessions; record i -> session i mod 65536, nonce (s << 32) + i div
+    65536 (nonce word 15 set), keys from splitmix64(0x4B4559)."""
+    S, per, L = 65536, 16, 1024
+    R = S * per
+    d_pt = torch.empty(R * L, dtype=torch.uint8, device="cuda")
+    noise_amd.fill_synthetic(d_pt, R * L, SEED)
+    d_keys = torch.empty(S * 32, dtype=torch.uint8, device="cuda")
+    noise_amd.fill_synthetic(d_keys, S * 32, 0x4B4559)
+    i = torch.arange(R, dtype=torch.int64, device="cuda")
+    d_idx = (i % S).to(torch.int32)
+    d_non = ((i % S) << 32) + i // S
+    d_ct = torch.empty(R * (L + 16), dtype=torch.uint8, device="cuda")
+    d_back = torch.empty(R * L, dtype=torch.uint8, device="cuda")
+    d_st = torch.full((R,), 9, dtype=torch.uint8, device="cuda")
+    noise_amd.encrypt_sessions(d_keys, S, d_idx, d_non, d_pt, L, d_ct, L + 16, L, R)
+    noise_amd.decrypt_sessions(d_keys, S, d_idx, d_non, d_ct, L + 16, d_back, L, L, d_st, R)
+    torch.cuda.synchronize()
+    assert int((d_st != 0).sum().item()) == 0, "a tag did not verify"
+    assert torch.equal(d_pt, d_back)
+    keys = _bytes(d_keys)
+    rng = random.Random(3)
+    for r in rng.sample(range(R), 300) + [0, S - 1, S, R - S, R - 1]:
+        s, n = r % S, ((r % S) << 32) + r // S
+        pt = _bytes(d_pt[r * L:(r + 1) * L])
+        want = oracle.encrypt(keys[32 * s:32 * s + 32], n, b"", pt)
+        assert _bytes(d_ct[r * (L + 16):(r + 1) * (L + 16)]) == want, r
+
+
+def test_config4_full_size_zipf(oracle):
+    """The exact bench batch: 2^20 records of 64 * 2^k bytes, P(k) ~ 1/(k+1),
+    top bucket 65519, packed at 16-byte aligned offsets, one key, nonces
+    0..R-1, through encrypt_records / decrypt_records (classifier, tile
+    classes, 1 KiB segments + tails + finalize, generic)."""
+    import bench
+    R = 1 << 20
+    lens = bench.zipf_lengths(R)
+    in_sz = (lens + np.uint64(15)) // np.uint64(16) * np.uint64(16)
+    ct_sz = (lens + np.uint64(31)) // np.uint64(16) * np.uint64(16)
+    in_off = np.concatenate([[0], np.cumsum(in_sz)[:-1]]).astype(np.uint64)
+    ct_off = np.concatenate([[0], np.cumsum(ct_sz)[:-1]]).astype(np.uint64)
+    enc = np.zeros(R, dtype=noise_amd.record_dtype())
+    enc["in_off"], enc["out_off"] = in_off, ct_off
+    enc["nonce"] = np.arange(R, dtype=np.uint64)
+    enc["len"] = lens
+    dec = enc.copy()
+    dec["in_off"], dec["out_off"] = ct_off, in_off
+    tot_in, tot_ct = int(in_sz.sum()), int(ct_sz.sum())
+    key = bytes(range(32))
+    d_pt = torch.empty(tot_in, dtype=torch.uint8, device="cuda")
+    noise_amd.fill_synthetic(d_pt, tot_in, SEED)
+    # zero the alignment padding so the whole buffers compare after the round trip
+    padn = (in_sz - lens).astype(np.int64)
+    starts = (in_off + lens).astype(np.int64)
+    pad_idx = np.repeat(starts, padn) + (np.arange(int(padn.sum())) -
+                                         np.repeat(np.cumsum(padn) - padn, padn))
+    d_pt[torch.from_numpy(pad_idx).cuda()] = 0
+    d_ct = torch.empty(tot_ct, dtype=torch.uint8, device="cuda")
+    d_back = torch.zeros(tot_in, dtype=torch.uint8, device="cuda")
+    d_st = torch.full((R,), 9, dtype=torch.uint8, device="cuda")
+    d_key = torch.frombuffer(bytearray(key), dtype=torch.uint8).cuda()
+    noise_amd.encrypt_records(d_key, 1, torch.from_numpy(enc.view(np.uint8).copy()).cuda(), R, d_pt, d_ct)
+    noise_amd.decrypt_records(d_key, 1, torch.from_numpy(dec.view(np.uint8).copy()).cuda(), R, d_ct,
+                              d_back, d_st)
+    torch.cuda.synchronize()
+    assert int((d_st != 0).sum().item()) == 0, "a tag did not verify"
+    assert torch.equal(d_pt, d_back)
+    rng = random.Random(4)
+    sample = set(rng.sample(range(R), 256)) | {0, R - 1}
+    for L in np.unique(lens):  # every length class, incl. all 65519-byte records up to 40
+        idx = np.nonzero(lens == L)[0]
+        sample |= set(int(x) for x in idx[:40])
+    for r in sorted(sample):
+        o, n, c = int(in_off[r]), int(lens[r]), int(ct_off[r])
+        want = oracle.encrypt(key, r, b"", _bytes(d_pt[o:o + n]))
+        assert _bytes(d_ct[c:c + n + 16]) == want, (r, n)
+    assert int((lens == 65519).sum()) > 1000
+
+
+def test_config5_full_size_shard(oracle):
+    """Config 5 at 1 GPU: 8 Mi x 4 KiB, one key, nonce = global index (the
+    strong-scaling N = 1 point; ~96 GiB resident), encrypt + decrypt."""
+    R, L = 8 << 20, 4096
+    key = bytes(range(32))
+    d_pt = torch.empty(R * L, dtype=torch.uint8, device="cuda")
+    noise_amd.fill_synthetic(d_pt, R * L, SEED)
+    d_ct = torch.empty(R * (L + 16), dtype=torch.uint8, device="cuda")
+    d_back = torch.empty(R * L, dtype=torch.uint8, device="cuda")
+    d_st = torch.full((R,), 9, dtype=torch.uint8, device="cuda")
+    noise_amd.encrypt_uniform(key, 0, d_pt, L, d_ct, L + 16, L, R)
+    noise_amd.decrypt_uniform(key, 0, d_ct, L + 16, d_back, L, L, d_st, R)
+    torch.cuda.synchronize()
+    assert int((d_st != 0).sum().item()) == 0, "a tag did not verify"
+    assert torch.equal(d_pt, d_back)
+    rng = random.Random(5)
+    for r in rng.sample(range(R), 256) + [0, R - 1]:
+        pt = _bytes(d_pt[r * L:(r + 1) * L])
+        assert pt == oracle.synthetic(L, SEED, offset=r * L)
+        assert _bytes(d_ct[r * (L + 16):(r + 1) * (L + 16)]) == oracle.encrypt(key, r, b"", pt), r

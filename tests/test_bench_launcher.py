@@ -61,3 +61,25 @@ def test_check_shards_flags_overlap():
     spans = [bench.shard(8 << 20, r, 8) for r in range(8)]
     assert spans[0][0] == 0 and spans[-1][1] == 8 << 20
     assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+
+
+@pytest.mark.parametrize("cfg", [2, 3, 5])
+def test_roofline_fields_from_committed_profiles(cfg):
+    """bench.py's roofline block is recomputable from profiles/: the kernel
+    symbol the driver's run launches, HBM traffic from the committed PMC
+    passes (gfx950 FETCH_SIZE correction), both HBM fractions and the VALU
+    issue fraction from SQ_INSTS_VALU."""
+    sys.path.insert(0, ROOT)
+    import bench
+    L = {2: 1024, 3: 1024, 5: 4096}[cfg]
+    mode = 1 if cfg == 3 else 0
+    R = 1 << 20
+    wl = {"enc_bytes": R * (2 * L + 16), "dec_bytes": R * (2 * L + 17), "read_bytes": (R * L, R * (L + 16)),
+          "knames": ((bench.tile_symbol(False, L, True, mode),), (bench.tile_symbol(True, L, True, mode),))}
+    roof = bench.roofline(cfg, wl, 0.61, 0.60)
+    assert roof["kernel"].startswith("noise_amd::k_aead_tile<false, %d, true, %d" % (L, mode))
+    assert roof["pmc_source"] and roof["pmc_source"].startswith("profiles/")
+    assert roof["traffic"] and 0.95 < roof["traffic"] / wl["enc_bytes"] < 1.2
+    assert 0 < roof["hbm_frac_read"] < roof["hbm_frac_rw"] < 1
+    v = roof["valu"]
+    assert v["insts_per_wave"] > 10000 and 0 < v["frac"] <= 1.2

@@ -283,7 +283,14 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
   constexpr bool SEG = MODE == kTileSeg;
   constexpr int OPR = (DECRYPT || SEG) ? C::SPR : C::SPR + 1;  // out pieces / record
   constexpr int OUT_SLOTS = C::RPT * OPR;
-  constexpr int NOUT = (OUT_SLOTS + 63) / 64;          // store instructions
+  // RECW (contiguous encrypt of records of >= 1 KiB): output instruction
+  // q < NDATA stores 64 ciphertext pieces of ONE record (swizzled LDS reads
+  // within one 64-slot group: bank-conflict free; destination uniform), the
+  // last one the tile's RPT tags.  Otherwise instruction q stores pieces
+  // 64q..64q+63 of the tile's output in wire order (ct || tag interleaved).
+  constexpr bool RECW = CONTIG && !DECRYPT && C::SPR >= 64 && C::SPR % 64 == 0;
+  constexpr int NDATA = C::RPT * C::SPR / 64;
+  constexpr int NOUT = RECW ? NDATA + 1 : (OUT_SLOTS + 63) / 64;  // store instructions
   static_assert(!(CONTIG && (MODE == kTileDesc || SEG)), "descriptor tiles are strided");
   static_assert(!SEG || (L == 1024 && SPAN == 256), "segments are 1 KiB, 256 B per lane");
   static_assert(NBUF == 1 || NBUF == 2, "one or two tile buffers");
@@ -574,6 +581,20 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     // destination, v_readlane), instruction RPT (encrypt) the RPT tags
     constexpr bool RECQ = SEG || (MODE == kTileDesc && C::SPR == 64);
     auto piece = [&](int q, uint32_t &r, uint32_t &pc, uint32_t &slot, bool &ok) {
+      if (RECW) {
+        if (q < NDATA) {
+          r = (uint32_t)q / (C::SPR / 64);
+          pc = 64u * ((uint32_t)q % (C::SPR / 64)) + lane;
+          slot = swz(64u * q + lane);  // == swz(r * SPR + pc)
+          ok = true;
+        } else {
+          r = lane < (uint32_t)C::RPT ? lane : 0u;
+          pc = C::SPR;
+          slot = C::REC_SLOTS + r;
+          ok = lane < (uint32_t)C::RPT;
+        }
+        return;
+      }
       if (RECQ) {
         if (q < C::RPT) {
           r = (uint32_t)q; pc = lane; slot = swz(64u * q + lane); ok = true;
@@ -664,7 +685,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
           dst = out + off + 16u * pc;
         } else {
           dst = out + rec0 * a.out_stride +
-                (CONTIG ? 16ull * g : r * a.out_stride + 16u * pc);
+                ((CONTIG && !RECW) ? 16ull * g : r * a.out_stride + 16u * pc);
         }
         if (store) store16<true>(dst, ov[qq], 16);
       }

@@ -135,9 +135,10 @@ int main() {
     }
     scan(big ? "encrypt_records_host (classified)" : "encrypt_records_host (small)");
   }
-  // ---- uniform batch between host buffers (pipeline)
-  {
-    const uint32_t L = 256, R = 300;
+  // ---- uniform batch between host buffers (pipeline; the tile kernel's
+  // wire-order gather below 1 KiB, the record-wise one from 1 KiB)
+  for (uint32_t L : {256u, 1024u, 4096u}) {
+    const uint32_t R = L >= 4096 ? 70 : 300;
     const auto pt = rbytes((size_t)L * R);
     std::vector<uint8_t> ct((size_t)(L + 16) * R), back((size_t)L * R), st(R, 9);
     double secs = 0;

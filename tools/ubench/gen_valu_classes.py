@@ -43,6 +43,56 @@ SINGLE = {
     "mad_u32_u16": "v_mad_u32_u16 v{d}, v{d}, v20, v{s}",
     "lshr_vv": "v_lshrrev_b32 v{d}, v21, v{d}",
     "mov_s": "v_mov_b32 v{d}, s20",
+    "cnd_vcc": "v_cndmask_b32_e32 v{d}, v{d}, v{s}, vcc",
+    "cnd_sgpr": "v_cndmask_b32_e64 v{d}, v{d}, v{s}, s[20:21]",
+    "addc": "v_addc_co_u32_e32 v{d}, vcc, v{d}, v{s}, vcc",
+}
+
+
+def pairs(fmt_list, n=64):
+    """repeat a short dependent sequence (e.g. an add-with-carry chain)"""
+    out = []
+    for i in range(n // len(fmt_list)):
+        d = (i * len(fmt_list)) % 16
+        for k, f in enumerate(fmt_list):
+            e = (2 * (d + k)) % 16
+            out.append(f.format(d=(d + k) % 16, s=(d + k + 8) % 16, t=(d + k + 4) % 16, d2=e, d3=e + 1))
+    return out
+
+
+CHAINS = {
+    # h + m with full carry propagation, then the carry materialised (poly_block as compiled)
+    "chain_add5_cnd": ["v_add_co_u32_e32 v{d}, vcc, v{d}, v{s}", "v_addc_co_u32_e32 v{d}, vcc, v{d}, v{s}, vcc",
+                       "v_addc_co_u32_e32 v{d}, vcc, v{d}, v{s}, vcc", "v_addc_co_u32_e32 v{d}, vcc, v{d}, v{s}, vcc",
+                       "v_cndmask_b32_e64 v{t}, 0, 1, vcc"],
+    "chain_add5_addc": ["v_add_co_u32_e32 v{d}, vcc, v{d}, v{s}", "v_addc_co_u32_e32 v{d}, vcc, v{d}, v{s}, vcc",
+                        "v_addc_co_u32_e32 v{d}, vcc, v{d}, v{s}, vcc", "v_addc_co_u32_e32 v{d}, vcc, v{d}, v{s}, vcc",
+                        "v_addc_co_u32_e32 v{t}, vcc, 1, v{t}, vcc"],
+    "xor_addc_mix": ["v_xor_b32_e32 v{t}, v{t}, v{s}", "v_addc_co_u32_e32 v{d}, vcc, v{d}, v{s}, vcc"],
+    "cnd_e64_vcc": ["v_cndmask_b32_e64 v{d}, v{d}, v{s}, vcc"],
+    "cmp_cnd_vcc": ["v_cmp_gt_u32_e32 vcc, v{d}, v{s}", "v_cndmask_b32_e64 v{t}, 0, 1, vcc"],
+    "cmp_cnd_sgpr": ["v_cmp_gt_u32_e64 s[20:21], v{d}, v{s}", "v_cndmask_b32_e64 v{t}, 0, 1, s[20:21]"],
+    "cmp_cnd_sgpr2": ["v_cmp_gt_u32_e64 s[20:21], v{d}, v{s}", "v_cmp_gt_u32_e64 s[22:23], v{s}, v{d}",
+                      "v_cndmask_b32_e64 v{t}, 0, 1, s[20:21]", "v_cndmask_b32_e64 v{d}, 0, 1, s[22:23]"],
+    "mad64_vcc": ["v_mad_u64_u32 v[16:17], vcc, v{d}, v{s}, v[16:17]"],
+    "mad64_sdst": ["v_mad_u64_u32 v[16:17], s[20:21], v{d}, v{s}, v[16:17]"],
+    "mad64_4acc_sdst": ["v_mad_u64_u32 v[16:17], s[20:21], v{d}, v{s}, v[16:17]",
+                        "v_mad_u64_u32 v[18:19], s[20:21], v{d}, v{t}, v[18:19]",
+                        "v_mad_u64_u32 v[24:25], s[20:21], v{s}, v{t}, v[24:25]",
+                        "v_mad_u64_u32 v[26:27], s[20:21], v{t}, v{d}, v[26:27]"],
+    "mad64_4acc_rot": ["v_mad_u64_u32 v[16:17], s[20:21], v{d}, v{s}, v[16:17]",
+                       "v_mad_u64_u32 v[18:19], s[22:23], v{d}, v{t}, v[18:19]",
+                       "v_mad_u64_u32 v[24:25], s[24:25], v{s}, v{t}, v[24:25]",
+                       "v_mad_u64_u32 v[26:27], s[26:27], v{t}, v{d}, v[26:27]"],
+    "xor_mad_mix": ["v_xor_b32_e32 v{t}, v{t}, v{s}", "v_mad_u64_u32 v[16:17], s[20:21], v{d}, v{s}, v[16:17]",
+                    "v_xor_b32_e32 v{d}, v{d}, v{s}", "v_mad_u64_u32 v[18:19], s[22:23], v{d}, v{t}, v[18:19]"],
+    "addc_4chains": ["v_add_co_u32_e64 v{d}, s[20:21], v{d}, v{s}", "v_add_co_u32_e64 v{t}, s[22:23], v{t}, v{s}",
+                     "v_add_co_u32_e64 v{s}, s[24:25], v{s}, v{d}", "v_add_co_u32_e64 v28, s[26:27], v28, v{d}",
+                     "v_addc_co_u32_e64 v{d}, s[20:21], v{d}, v{s}, s[20:21]",
+                     "v_addc_co_u32_e64 v{t}, s[22:23], v{t}, v{s}, s[22:23]",
+                     "v_addc_co_u32_e64 v{s}, s[24:25], v{s}, v{d}, s[24:25]",
+                     "v_addc_co_u32_e64 v28, s[26:27], v28, v{d}, s[26:27]"],
+    "lshl_add64": ["v_lshl_add_u64 v[16:17], v[{d2}:{d3}], 0, v[16:17]"],
 }
 
 
@@ -95,15 +145,17 @@ def qr_mad24(groups=2, rot7="fast"):
 VARIANTS = {"qr_alignbit": qr_alignbit(), "qr_mad24": qr_mad24(), "qr_mad24_r7ab": qr_mad24(rot7="alignbit")}
 for k, v in SINGLE.items():
     VARIANTS["1_" + k] = single(v)
+for k, v in CHAINS.items():
+    VARIANTS[k] = pairs(v, 60)
 
 HDR = r'''#include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
 #define ITERS 2048
 '''
-CLOB = ",".join('"v%d"' % i for i in range(32)) + ',"s20"'
+CLOB = ",".join('"v%d"' % i for i in range(32)) + ',"s20","s21","s22","s23","s24","s25","s26","s27","vcc"'
 SETUP = ("v_mov_b32 v20, 0x10000\\n\\tv_mov_b32 v21, 0x1000\\n\\tv_mov_b32 v22, 0x100\\n\\t"
-         "v_mov_b32 v23, 0x80\\n\\ts_mov_b32 s20, 0x10000")
+         "v_mov_b32 v23, 0x80\\n\\ts_mov_b32 s20, 0x10000\\n\\ts_mov_b32 s21, 0")
 
 
 def kernel(name, insts):

@@ -22,6 +22,7 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <memory>
 #include <vector>
 
 #include "noise_amd/cipher_state.hpp"
@@ -92,7 +93,9 @@ class Batcher {
 // A Batch view stays valid until its slot is refilled, i.e. until `depth - 1`
 // further flushes; flush() blocks only when the slot it moves on to is still
 // in flight (back-pressure).  Session keys are uploaded to a device key table
-// once, when the session is added; not thread-safe (like CipherState).
+// once, when the session is added.  One thread drives a Pipeline (like
+// CipherState); submit_batch / copy_out fan the byte copies out to an
+// internal pool of Options::copy_threads threads.
 class Pipeline {
  public:
   using Direction = Batcher::Direction;
@@ -100,6 +103,13 @@ class Pipeline {
     std::size_t slot_bytes = std::size_t(32) << 20;  // message bytes per slot
     std::size_t slot_records = std::size_t(1) << 16; // messages per slot
     int depth = 3;                                   // slots in the ring
+    int copy_threads = 1;  // host threads copying messages in / results out
+                           // (submit_batch, copy_out); 1 = the caller only
+  };
+  struct Message {
+    std::size_t session;
+    const std::uint8_t *data;
+    std::size_t len;
   };
   class Batch {
    public:
@@ -127,6 +137,15 @@ class Pipeline {
   // copy one message into the filling slot and assign its nonce; false (and
   // nothing consumed) when the slot has no room -- flush() and retry
   bool submit(std::size_t s, const std::uint8_t *msg, std::size_t len);
+  // Queue the longest prefix of messages[0..n) that fits the filling slot,
+  // exactly as that many submit() calls would (nonces in order per session,
+  // the same length / nonce-limit exceptions), with the byte copies spread
+  // over Options::copy_threads threads.  Returns how many were queued; 0
+  // means the slot is full: flush() and call again.
+  std::size_t submit_batch(const Message *messages, std::size_t n);
+  // copy a waited batch's results out (dst[i] <- data(i), length(i) bytes),
+  // over Options::copy_threads threads
+  void copy_out(const Batch &b, std::uint8_t *const *dst);
   [[nodiscard]] std::size_t pending() const;
   // launch the filling slot; its ticket (0 if it was empty)
   std::uint64_t flush();
@@ -150,6 +169,8 @@ class Pipeline {
   std::size_t key_cap_ = 0, key_dirty_ = 0;
   void *keys_evt_ = nullptr;  // hipEvent_t: latest key-row upload (any slot stream)
   bool keys_uploaded_ = false;
+  struct CopyPool;
+  std::unique_ptr<CopyPool> pool_;
 };
 
 }  // namespace noise::transport

@@ -2,10 +2,14 @@
 // descriptor-batch C ABI (noise_amd/transport.hpp).
 #include "noise_amd/transport.hpp"
 
+#include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <limits>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 
 #include <hip/hip_runtime_api.h>
 
@@ -118,6 +122,70 @@ inline std::size_t align16(std::size_t x) { return (x + 15) & ~std::size_t(15); 
 inline std::size_t align256(std::size_t x) { return (x + 255) & ~std::size_t(255); }
 }  // namespace
 
+// Fork-join pool for the host byte copies (submit_batch / copy_out): the
+// caller runs chunk 0 of every job, workers 1..T-1 the others.
+struct Pipeline::CopyPool {
+  explicit CopyPool(int threads) : nthr(threads < 1 ? 1 : threads) {
+    for (int w = 1; w < nthr; ++w) th.emplace_back([this, w] { worker(w); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto &t : th) t.join();
+  }
+  // fn(lo, hi) over [0, n) in nthr contiguous chunks
+  void run(std::size_t n, const std::function<void(std::size_t, std::size_t)> &fn) {
+    if (nthr == 1 || n < 64) {
+      fn(0, n);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      job = &fn;
+      total = n;
+      pending = nthr - 1;
+      ++gen;
+    }
+    cv.notify_all();
+    fn(0, n / nthr);
+    std::unique_lock<std::mutex> lk(mu);
+    done.wait(lk, [this] { return pending == 0; });
+    job = nullptr;
+  }
+  void worker(int w) {
+    std::uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(std::size_t, std::size_t)> *fn;
+      std::size_t n;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return stop || gen != seen; });
+        if (stop) return;
+        seen = gen;
+        fn = job;
+        n = total;
+      }
+      (*fn)(n * w / nthr, n * (w + 1) / nthr);
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        if (--pending == 0) done.notify_one();
+      }
+    }
+  }
+  int nthr;
+  std::vector<std::thread> th;
+  std::mutex mu;
+  std::condition_variable cv, done;
+  const std::function<void(std::size_t, std::size_t)> *job = nullptr;
+  std::size_t total = 0;
+  std::uint64_t gen = 0;
+  int pending = 0;
+  bool stop = false;
+};
+
 // One ring slot: pinned host image and device image of
 // [records | message bytes in | message bytes out | status]
 struct Pipeline::Slot {
@@ -146,6 +214,7 @@ Pipeline::Pipeline(Direction d, const Options &o) : dir_(d), opt_(o) {
     hip_check(hipStreamCreateWithFlags(&sl->st, hipStreamNonBlocking), "slot stream");
     hip_check(hipEventCreateWithFlags(&sl->done, hipEventDisableTiming), "slot event");
   }
+  pool_ = std::make_unique<CopyPool>(opt_.copy_threads);
   hipEvent_t ke = nullptr;
   hip_check(hipEventCreateWithFlags(&ke, hipEventDisableTiming), "key event");
   keys_evt_ = ke;
@@ -244,6 +313,55 @@ bool Pipeline::submit(std::size_t s, const std::uint8_t *msg, std::size_t len) {
   ++sl.nrec;
   ++n;  // decrypt: advances whatever the tag says (noise.cpp:421)
   return true;
+}
+
+std::size_t Pipeline::submit_batch(const Message *messages, std::size_t n) {
+  const bool dec = dir_ == Direction::Decrypt;
+  Slot &sl = *slots_[fill_];
+  // 1. bookkeeping in order (cheap): nonces, offsets, descriptors
+  std::size_t k = 0, in_used = sl.in_used, out_used = sl.out_used;
+  for (; k < n; ++k) {
+    const Message &m = messages[k];
+    // a refused message stops the batch before it; it throws when it comes first
+    // (as its submit() would), so the messages ahead of it are never lost
+    const bool bad_nonce = m.session >= nonces_.size() ||
+                           nonces_[m.session] == std::numeric_limits<std::uint64_t>::max() - 1;
+    const bool bad_len = dec ? (m.len < 16 || m.len > kMaxMessage) : m.len + 16 > kMaxMessage;
+    if (bad_nonce || bad_len) {
+      if (k > 0) break;
+      const std::uint64_t nn = nonces_.at(m.session);
+      if (nn == std::numeric_limits<std::uint64_t>::max() - 1)  // noise.cpp:398-400
+        throw std::out_of_range("Nonce limit has been exceeded!");
+      if (!dec) throw std::length_error("Noise message exceeds 65535 bytes");
+      throw std::invalid_argument("Invalid MAC");
+    }
+    const std::uint64_t nn = nonces_[m.session];
+    const std::size_t in_len = align16(m.len), out_len = dec ? align16(m.len - 16) : align16(m.len + 16);
+    if (sl.nrec + k == opt_.slot_records || in_used + in_len > opt_.slot_bytes) break;
+    sl.recs()[sl.nrec + k] = noise_gpu_record{in_used, out_used, nn, 0,
+                                             (std::uint32_t)(dec ? m.len - 16 : m.len), 0,
+                                             (std::uint32_t)m.session, 0};
+    ++nonces_[m.session];  // decrypt: advances whatever the tag says (noise.cpp:421)
+    in_used += in_len;
+    out_used += out_len;
+  }
+  // 2. the byte copies, in parallel
+  const std::size_t base = sl.nrec;
+  pool_->run(k, [&](std::size_t lo, std::size_t hi) {
+    for (std::size_t i = lo; i < hi; ++i)
+      if (messages[i].len)
+        std::memcpy(sl.h + o_in_ + sl.recs()[base + i].in_off, messages[i].data, messages[i].len);
+  });
+  sl.nrec += k;
+  sl.in_used = in_used;
+  sl.out_used = out_used;
+  return k;
+}
+
+void Pipeline::copy_out(const Batch &b, std::uint8_t *const *dst) {
+  pool_->run(b.size(), [&](std::size_t lo, std::size_t hi) {
+    for (std::size_t i = lo; i < hi; ++i) std::memcpy(dst[i], b.data(i), b.length(i));
+  });
 }
 
 std::uint64_t Pipeline::flush() {

@@ -10,8 +10,9 @@
 //       uploads a large table of new sessions' keys, slot B (another stream,
 //       no upload of its own) is flushed right after with messages of the
 //       last sessions; B's ciphertexts must match the oracle
-//   transport_test bench <batcher|pipeline> <sessions> <messages> <len>
-//       host-resident throughput, encrypt then decrypt, GiB/s of plaintext
+//   transport_test bench <batcher|pipeline> <sessions> <messages> <len> [threads]
+//       host-resident throughput, encrypt then decrypt, GiB/s of plaintext;
+//       threads > 1: Pipeline::submit_batch / copy_out over that many copy threads
 // Sessions get random keys and start nonces; messages (0..2000 bytes, some
 // 65519) are submitted interleaved, encrypted in ONE batch, checked bit-exact
 // against oracle_noise_encrypt with each session's nonce sequence, framed per
@@ -156,6 +157,96 @@ static int run_pipeline(int S, int M, std::uint64_t seed) {
   return fails ? 1 : 0;
 }
 
+// Pipeline::submit_batch / copy_out (4 copy threads): ragged chunks of
+// messages (1..300, crossing slot boundaries), ciphertexts vs the oracle,
+// then decrypt back through batches with tampered records.
+static int run_pipeline_batch(int S, int M, std::uint64_t seed) {
+  std::mt19937_64 rng(seed);
+  int fails = 0;
+  auto check = [&](bool c, const char *what, long i) {
+    if (!c && fails++ < 20) std::printf("FAIL %s (%ld)\n", what, i);
+  };
+  nt::Pipeline::Options o;
+  o.slot_bytes = 256 << 10;
+  o.slot_records = 97;
+  o.depth = 3;
+  o.copy_threads = 4;
+  nt::Pipeline enc(nt::Pipeline::Direction::Encrypt, o), dec(nt::Pipeline::Direction::Decrypt, o);
+  std::vector<std::array<std::uint8_t, 32>> keys(S);
+  std::vector<std::uint64_t> n0(S);
+  for (int s = 0; s < S; ++s) {
+    for (auto &b : keys[s]) b = (std::uint8_t)rng();
+    n0[s] = rng() % 1000;
+    noise::CipherState cs;
+    cs.initialize_key(keys[s]);
+    cs.set_nonce(n0[s]);
+    enc.add_session(cs);
+    dec.add_session(cs);
+  }
+  std::vector<bytes> pt(M), ct(M), back(M);
+  std::vector<nt::Pipeline::Message> msgs(M);
+  for (int i = 0; i < M; ++i) {
+    pt[i].resize(rng() % 29 == 0 ? 65519 : rng() % 3000);
+    for (auto &b : pt[i]) b = (std::uint8_t)rng();
+    msgs[i] = {(std::size_t)(rng() % S), pt[i].data(), pt[i].size()};
+  }
+  // one direction through the ring: batches of random size, results copied out
+  auto run = [&](nt::Pipeline &p, std::vector<bytes> &out, bool decrypt, std::vector<bool> *okv) {
+    std::deque<std::pair<std::uint64_t, int>> q;
+    std::vector<std::uint8_t *> dst(o.slot_records);
+    auto take = [&](std::size_t keep) {
+      while (q.size() > keep) {
+        auto [t, f] = q.front();
+        q.pop_front();
+        const nt::Pipeline::Batch b = p.wait(t);
+        for (std::size_t j = 0; j < b.size(); ++j) {
+          out[f + j].assign(b.length(j), 0);
+          dst[j] = out[f + j].data();
+          if (okv) (*okv)[f + j] = b.ok(j);
+        }
+        p.copy_out(b, dst.data());
+      }
+    };
+    int i = 0, first = 0;
+    while (i < M) {
+      const int want = std::min<int>(M - i, 1 + (int)(rng() % 300));
+      const std::size_t k = p.submit_batch(msgs.data() + i, (std::size_t)want);
+      i += (int)k;
+      if (k < (std::size_t)want) {
+        q.push_back({p.flush(), first});
+        first = i;
+        take(o.depth - 2);
+      }
+    }
+    if (p.pending()) q.push_back({p.flush(), first});
+    take(0);
+    (void)decrypt;
+  };
+  run(enc, ct, false, nullptr);
+  std::vector<std::uint64_t> next(n0);
+  bytes w(65535 + 16);
+  for (int i = 0; i < M; ++i) {
+    const std::size_t s = msgs[i].session;
+    oracle_noise_encrypt(keys[s].data(), next[s]++, nullptr, 0, pt[i].data(), pt[i].size(), w.data());
+    check(ct[i].size() == pt[i].size() + 16 && std::memcmp(ct[i].data(), w.data(), ct[i].size()) == 0,
+          "batched ciphertext vs oracle", i);
+  }
+  for (int s = 0; s < S; ++s) check(enc.nonce(s) == next[s], "batched nonce advance", s);
+  for (int i = 0; i < M; ++i) {
+    if (i % 71 == 9) ct[i][rng() % ct[i].size()] ^= 0x02;
+    msgs[i].data = ct[i].data();
+    msgs[i].len = ct[i].size();
+  }
+  std::vector<bool> okv(M);
+  run(dec, back, true, &okv);
+  for (int i = 0; i < M; ++i) {
+    if (i % 71 == 9) check(!okv[i], "batched tampered rejected", i);
+    else check(okv[i] && back[i] == pt[i], "batched decrypt round trip", i);
+  }
+  std::printf("pipeline_batch sessions %d messages %d: %s (%d failures)\n", S, M, fails ? "FAIL" : "ok", fails);
+  return fails ? 1 : 0;
+}
+
 static int run_keyrace(int S) {
   int fails = 0;
   std::mt19937_64 rng(99);
@@ -197,7 +288,7 @@ static int run_keyrace(int S) {
 
 // Host-resident throughput: M messages of len bytes from one source buffer
 // (the "socket reads"), encrypt then decrypt, results checksummed (touched).
-static int run_bench(const std::string &mode, int S, long M, std::size_t len) {
+static int run_bench(const std::string &mode, int S, long M, std::size_t len, int threads = 1) {
   std::mt19937_64 rng(7);
   bytes src((std::size_t)M * len);
   for (std::size_t i = 0; i < src.size(); i += 8) {
@@ -213,10 +304,12 @@ static int run_bench(const std::string &mode, int S, long M, std::size_t len) {
   using clk = std::chrono::steady_clock;
   std::uint64_t sum = 0;
   double secs[2] = {0, 0};
-  bytes ctall((std::size_t)M * (len + 16));
+  bytes ctall((std::size_t)M * (len + 16)), ptall(threads > 1 ? (std::size_t)M * len : 0);
   // long-lived objects, as in a server: built (pinned slots, key upload)
   // outside the timed region
-  nt::Pipeline penc(nt::Pipeline::Direction::Encrypt), pdec(nt::Pipeline::Direction::Decrypt);
+  nt::Pipeline::Options popt;
+  popt.copy_threads = threads;
+  nt::Pipeline penc(nt::Pipeline::Direction::Encrypt, popt), pdec(nt::Pipeline::Direction::Decrypt, popt);
   for (int s = 0; s < S; ++s) {
     penc.add_session(cs[s]);
     pdec.add_session(cs[s]);
@@ -240,6 +333,38 @@ static int run_bench(const std::string &mode, int S, long M, std::size_t len) {
             sum += r[j].msg[0];
           }
         }
+      } else if (threads > 1) {  // batched submit / copy-out over the pipeline's copy threads
+        nt::Pipeline &p = dec ? pdec : penc;
+        std::deque<std::pair<std::uint64_t, long>> q;
+        std::vector<nt::Pipeline::Message> msgs(M);
+        for (long i = 0; i < M; ++i) msgs[i] = {(std::size_t)(i % S), in + i * ilen, ilen};
+        std::vector<std::uint8_t *> dst(1 << 16);
+        auto take = [&](std::size_t keep) {
+          while (q.size() > keep) {
+            auto [t, f] = q.front();
+            q.pop_front();
+            const nt::Pipeline::Batch b = p.wait(t);
+            // results consumed: every message copied out (as a send() would), in parallel
+            for (std::size_t j = 0; j < b.size(); ++j)
+              dst[j] = dec ? ptall.data() + (f + j) * len : ctall.data() + (f + j) * (len + 16);
+            p.copy_out(b, dst.data());
+            if (dec)
+              for (std::size_t j = 0; j < b.size(); ++j)
+                if (!b.ok(j)) throw std::runtime_error("bench: decrypt failed");
+          }
+        };
+        long i = 0, first = 0;
+        while (i < M) {
+          const std::size_t k = p.submit_batch(msgs.data() + i, (std::size_t)(M - i));
+          i += (long)k;
+          if (i < M) {
+            q.push_back({p.flush(), first});
+            first = i;
+            take(1);
+          }
+        }
+        q.push_back({p.flush(), first});
+        take(0);
       } else {
         nt::Pipeline &p = dec ? pdec : penc;
         std::deque<std::pair<std::uint64_t, long>> q;
@@ -272,10 +397,14 @@ static int run_bench(const std::string &mode, int S, long M, std::size_t len) {
       if (pass > 0) secs[d] += t;
     }
   }
+  if (threads > 1) {  // the copied-out results, checked once outside the timed region
+    if (ptall != src) throw std::runtime_error("bench: batched round trip differs");
+    for (long i = 0; i < M; ++i) sum += ctall[(std::size_t)i * (len + 16)] + ptall[(std::size_t)i * len];
+  }
   const double gib = (double)M * len * 2 / (1u << 30);  // two timed passes per direction
-  std::printf("{\"mode\": \"%s\", \"sessions\": %d, \"messages\": %ld, \"len\": %zu, "
-              "\"encrypt_gib_s\": %.2f, \"decrypt_gib_s\": %.2f, \"checksum\": %llu}\n",
-              mode.c_str(), S, M, len, gib / secs[0], gib / secs[1], (unsigned long long)sum);
+  std::printf("{\"mode\": \"%s\", \"copy_threads\": %d, \"sessions\": %d, \"messages\": %ld, "
+              "\"len\": %zu, \"encrypt_gib_s\": %.2f, \"decrypt_gib_s\": %.2f, \"checksum\": %llu}\n",
+              mode.c_str(), threads, S, M, len, gib / secs[0], gib / secs[1], (unsigned long long)sum);
   return 0;
 }
 
@@ -283,8 +412,11 @@ int main(int argc, char **argv) {
   if (argc > 1 && std::string(argv[1]) == "pipeline")
     return run_pipeline(std::atoi(argv[2]), std::atoi(argv[3]), std::strtoull(argv[4], nullptr, 0));
   if (argc > 1 && std::string(argv[1]) == "keyrace") return run_keyrace(std::atoi(argv[2]));
+  if (argc > 1 && std::string(argv[1]) == "pipeline_batch")
+    return run_pipeline_batch(std::atoi(argv[2]), std::atoi(argv[3]), std::strtoull(argv[4], nullptr, 0));
   if (argc > 1 && std::string(argv[1]) == "bench")
-    return run_bench(argv[2], std::atoi(argv[3]), std::atol(argv[4]), std::strtoul(argv[5], nullptr, 0));
+    return run_bench(argv[2], std::atoi(argv[3]), std::atol(argv[4]), std::strtoul(argv[5], nullptr, 0),
+                     argc > 6 ? std::atoi(argv[6]) : 1);
   const int S = argc > 1 ? std::atoi(argv[1]) : 100;
   const int M = argc > 2 ? std::atoi(argv[2]) : 1000;
   std::mt19937_64 rng(argc > 3 ? std::strtoull(argv[3], nullptr, 0) : 1);

@@ -433,6 +433,18 @@ def test_transport_pipeline(sessions, messages, seed):
     assert "ok (0 failures)" in r.stdout
 
 
+@pytest.mark.parametrize("sessions,messages,seed", [(60, 2500, 5)])
+def test_transport_pipeline_batched_copies(sessions, messages, seed):
+    """Pipeline::submit_batch / copy_out with 4 copy threads: ragged batches
+    crossing slot boundaries, ciphertexts vs the oracle, nonce accounting,
+    decrypt round trip with tampered records rejected."""
+    exe = os.path.join(noise_amd.ROOT, "noise-cpp_amd", "bin", "transport_test")
+    r = subprocess.run([exe, "pipeline_batch", str(sessions), str(messages), str(seed)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "ok (0 failures)" in r.stdout
+
+
 def test_transport_pipeline_key_upload_order():
     """Pipeline key table: slot A uploads 2^18 new sessions'
     key rows (8 MiB) on its stream; slot B, flushed immediately on another

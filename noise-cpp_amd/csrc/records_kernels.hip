@@ -722,7 +722,7 @@ static inline unsigned capped(uint64_t want, uint64_t cap) {
 // on the companion stream while the segment kernel fills the GPU.
 struct AuxStream {
   hipStream_t aux = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
+  hipEvent_t fork = nullptr, prep = nullptr, join = nullptr;
 };
 static hipError_t aux_get(AuxStream *out, hipStream_t stream) {
   struct Entry {
@@ -745,19 +745,22 @@ static hipError_t aux_get(AuxStream *out, hipStream_t stream) {
   if ((e = hipStreamCreateWithFlags(&a.aux, hipStreamNonBlocking)) != hipSuccess) return e;
   if ((e = hipEventCreateWithFlags(&a.fork, hipEventDisableTiming)) != hipSuccess) return e;
   if ((e = hipEventCreateWithFlags(&a.join, hipEventDisableTiming)) != hipSuccess) return e;
+  if ((e = hipEventCreateWithFlags(&a.prep, hipEventDisableTiming)) != hipSuccess) return e;
   cache.push_back({dev, stream, a});
   *out = a;
   return hipSuccess;
 }
 
-// After the classifier, two branches (both read only the classifier's output):
-//   caller stream : k_seg_prep -> segment tile kernel ------ join -> finalize
-//                                                                  (-> fixup)
-//   companion     : (fork after prep) tails, the five small tile classes,
-//                   the generic kernel ----------------------^
+// After the classifier, two branches:
+//   caller stream : k_seg_prep -+-> segment tile kernel ----- join -> finalize
+//                               |                                   (-> fixup)
+//   companion     : (fork)  the five small tile classes, the generic kernel,
+//                   (wait prep) the tails ------------------------^
 // The segment kernel is the long pole (~80 % of a config-4 call); the
 // companion branch's launches are short or under-filled (the tails kernel has
-// one lane per tail) and now overlap it instead of following it.
+// one lane per tail) and overlap it instead of following it.  The tails go
+// last so their long per-lane chains fill the segment kernel's drain
+// (profiles/round2/ab/ab_experiments.md).
 template <bool DECRYPT>
 static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr *hdr,
                                  const uint8_t *keys, uint32_t nkeys,
@@ -772,11 +775,14 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   const dim3 bt(64);
   const dim3 grid(capped((nrec + 63) / 64, NOISE_GRID_CAP));
   SegRec *rt = const_cast<SegRec *>(ta.rt);
-  hipLaunchKernelGGL(k_seg_prep, grid, bt, 0, stream, keys, rt, hdr);
+  // fork right after the classifier: the small classes and the generic
+  // kernel need nothing else; the tails also need k_seg_prep (prep event)
   if ((e = hipEventRecord(ax.fork, stream)) != hipSuccess) return e;
   if ((e = hipStreamWaitEvent(ax.aux, ax.fork, 0)) != hipSuccess) return e;
-  // companion branch
-  hipLaunchKernelGGL((k_seg_tail<DECRYPT>), grid, bt, 0, ax.aux, tails, rt, hdr, in, out);
+  hipLaunchKernelGGL(k_seg_prep, grid, bt, 0, stream, keys, rt, hdr);
+  if ((e = hipEventRecord(ax.prep, stream)) != hipSuccess) return e;
+  // companion branch: dense tile classes first, the long-latency tails last
+  // (they then overlap the segment kernel's drain; tails first: -3..5 %)
   TileArgs a = ta;
 #define NOISE_DESC_TILE(C, LEN)                                                \
   a.cls = C;                                                                   \
@@ -792,6 +798,8 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   const dim3 gg((unsigned)(gblocks < 2 * NOISE_GRID_CAP ? gblocks : 2 * NOISE_GRID_CAP));
   hipLaunchKernelGGL((k_aead_records<DECRYPT>), gg, dim3(kGenBlock), 0, ax.aux, keys, nkeys, recs,
                      nrec, idx, hdr, in, out, ad, status);
+  if ((e = hipStreamWaitEvent(ax.aux, ax.prep, 0)) != hipSuccess) return e;
+  hipLaunchKernelGGL((k_seg_tail<DECRYPT>), grid, bt, 0, ax.aux, tails, rt, hdr, in, out);
   if ((e = hipEventRecord(ax.join, ax.aux)) != hipSuccess) return e;
   // caller-stream branch: every full segment of every long record
   const dim3 gseg(capped((segbound + 63) / 64, NOISE_GRID_CAP));

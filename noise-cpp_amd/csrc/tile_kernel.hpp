@@ -164,12 +164,24 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
     // records put piece g of an encrypt tile at byte 16g and of a decrypt
     // tile (SPR+1 pieces per record) at 16(g + g/SPR).
     const uint8_t *base = in + rec0 * in_stride;  // wave-uniform
+    if (nv >= (uint32_t)C::RPT) {
+      // full tile (every tile but a batch's last): no per-instruction guard,
+      // which the compiler otherwise turns into a compare, an exec mask and
+      // two taken branches around each of the REC_SLOTS / 64 DMAs
 #pragma unroll
-    for (int q = 0; q < C::REC_SLOTS / 64; ++q) {
-      const uint32_t g = 64u * q + gl[q & 3];
-      const uint32_t rr = g / C::SPR;
-      const uint32_t off = DECRYPT ? 16u * (g + rr) : 16u * g;
-      if (rr < nv) lds_dma16_s(base, off, (lds_void *)(lds3 + 64 * q));
+      for (int q = 0; q < C::REC_SLOTS / 64; ++q) {
+        const uint32_t g = 64u * q + gl[q & 3];
+        const uint32_t rr = g / C::SPR;
+        lds_dma16_s(base, DECRYPT ? 16u * (g + rr) : 16u * g, (lds_void *)(lds3 + 64 * q));
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < C::REC_SLOTS / 64; ++q) {
+        const uint32_t g = 64u * q + gl[q & 3];
+        const uint32_t rr = g / C::SPR;
+        const uint32_t off = DECRYPT ? 16u * (g + rr) : 16u * g;
+        if (rr < nv) lds_dma16_s(base, off, (lds_void *)(lds3 + 64 * q));
+      }
     }
     if (TAGGED_IN) {  // tag pieces: slot REC_SLOTS + r <- piece (r, SPR)
 #pragma unroll

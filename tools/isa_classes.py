@@ -90,6 +90,7 @@ def main():
     static = collections.Counter()
     per_depth = collections.defaultdict(collections.Counter)
     hot_ops = collections.Counter()
+    by_class = collections.defaultdict(collections.Counter)
     for label, d, c, o in blocks:
         static.update(c)
         per_depth[d].update(c)
@@ -100,12 +101,14 @@ def main():
             dyn[k] += v * mult
         for k, v in o.items():
             hot_ops[k] += v * mult
+            by_class[classify(k, k)][k] += v * mult
     valu = sum(v for k, v in dyn.items() if k in ("arx", "mul", "carry_select", "valu_other", "cross_lane"))
     out = {"symbol": sym, "trips": {"depth1": trips[1], "depth2": trips[2]},
            "static_by_class": dict(static),
            "static_by_depth": {str(d): dict(c) for d, c in sorted(per_depth.items())},
            "dynamic_per_wave": dict(dyn), "dynamic_valu_per_wave": valu,
            "top_ops_dynamic": dict(hot_ops.most_common(40)),
+           "ops_by_class_dynamic": {c: dict(o.most_common()) for c, o in sorted(by_class.items())},
            "cold_blocks": sorted(cold)}
     print(json.dumps(out, indent=1))
 

@@ -74,14 +74,18 @@ const char *noise_gpu_last_error(void);
 int noise_gpu_device_count(int *count);
 
 /* ---- device-resident uniform batches (the BASELINE hot path) -----------
- * nrec records of exactly `len` plaintext bytes under one 32-byte key.
+ * nrec records of exactly `len` plaintext bytes under one 32-byte key (an
+ * all-zero key is "no key", Noise HasKey() false, and is refused with
+ * NOISE_GPU_E_ARG rather than used as a publicly known key).
  * Record i: input at d_in + i*in_stride, output at d_out + i*out_stride,
  * associated data at d_ad + i*ad_stride (ad_stride 0 = the same AD for every
  * record; ad_len 0 = no AD, the transport case).
  * Encrypt writes len+16 bytes per record (ct || tag).  in == out with equal
  * strides is in-place; other overlaps are undefined.
  * Decrypt reads len+16 bytes per record, writes len plaintext bytes only
- * where the tag verifies, and writes d_status[i] (NOISE_GPU_REC_*).  A
+ * where the tag verifies (both the tile kernel and the one-lane-per-record
+ * path check the tag before storing any plaintext), and writes d_status[i]
+ * (NOISE_GPU_REC_*).  A
  * record whose tag fails is left as it was when in-place (the reference
  * leaves the buffer untouched, monocypher.c:2919-2926) and is zeroed in an
  * out-of-place output (no unauthenticated plaintext is left behind).
@@ -107,18 +111,24 @@ int noise_gpu_decrypt_uniform(const uint8_t h_key[32], uint64_t nonce0,
  * d_keys: [nkeys][32] key table in HBM (16-byte aligned); d_recs: nrec
  * descriptors in HBM.  Same in-place / failure rules as the uniform
  * functions; a record is in place when d_in + in_off == d_out + out_off.
- * A descriptor whose key_idx >= nkeys is not processed (nothing written;
- * decrypt status NOISE_GPU_REC_BAD_KEY).
+ * A descriptor whose key_idx >= nkeys, or whose key row is all zero (the
+ * "no key" row noise_gpu_hs_split gives a failed handshake), is not processed
+ * (nothing written; decrypt status NOISE_GPU_REC_BAD_KEY).
  * Batches of >= 2048 records are load-balanced on the device, stream-ordered
  * (no host synchronisation): records are sorted by class and each class
  * runs its own kernel -- 16-byte aligned AD-free records of 64, 128, 192,
  * 256 and 512 bytes on the LDS-staged tile kernel; aligned AD-free records of
  * 1024..65535 bytes (any length) cut into 1 KiB segments that ONE tile-kernel
  * launch processes, plus a tail kernel and a per-record finalize (tag);
- * everything else one lane per record.  Decrypt of a segmented record writes
- * plaintext before its tag is checked and restores (in place) or zeroes
- * (copy) it when the tag fails, so the final buffer contents follow the rules
- * above.  Scratch is a grow-only device buffer per (device, stream). */
+ * everything else one lane per record.  The tile classes and the
+ * one-lane-per-record path check each tag before they store plaintext.  A
+ * segmented (>= 1 KiB) record is the exception: its segments are decrypted
+ * in parallel before the record's tag is known, so the plaintext is written
+ * first and, when the tag fails, XORed back to the ciphertext (in place) or
+ * zeroed (copy) by a fix-up kernel later in the same call.  The final buffer
+ * contents follow the rules above; between those kernels the output buffer
+ * transiently holds unauthenticated plaintext of a failed record.  Scratch
+ * is a grow-only device buffer per (device, stream). */
 int noise_gpu_encrypt_records(const uint8_t *d_keys, uint32_t nkeys,
                               const noise_gpu_record *d_recs, uint64_t nrec,
                               const uint8_t *d_in, uint8_t *d_out,
@@ -145,8 +155,9 @@ int noise_gpu_scratch_wipe(void *stream);
  * Served by the LDS-staged tile kernel: len in {64, 128, 192, 256, 512,
  * 1024, 2048, 4096, 8192, 16384} with 16-byte aligned buffers/strides; other shapes
  * return NOISE_GPU_E_ARG (use the descriptor functions below).  A record
- * whose key index is >= nkeys is not written; decrypt marks it
- * NOISE_GPU_REC_BAD_KEY. */
+ * whose key index is >= nkeys, or whose key row is all zero, is not written;
+ * decrypt marks it NOISE_GPU_REC_BAD_KEY.  Tags are checked before any
+ * plaintext is stored. */
 #define NOISE_GPU_REC_BAD_KEY 2u
 int noise_gpu_encrypt_sessions(const uint8_t *d_keys, uint32_t nkeys,
                                const uint32_t *d_key_idx,
@@ -265,11 +276,17 @@ int noise_gpu_hs_split(noise_gpu_hs *hs, uint8_t *d_k1, uint8_t *d_k2,
 
 /* ---- host-buffer entry points (synchronous) ----------------------------
  * Used by the CipherState shim for single records (encrypt_with_ad /
- * decrypt_with_ad / rekey).  They stage through pinned host memory and a
- * per-thread device scratch area, run the same kernels and synchronise.
- * h_buf holds len plaintext bytes and has room for len+16 (encrypt), or
- * holds ct_len = len+16 bytes (decrypt, plaintext written to h_buf[0..len)
- * on success, h_buf untouched and NOISE_GPU_E_MAC returned on failure). */
+ * decrypt_with_ad / rekey).  A record of <= 65535 bytes with <= 8192 bytes of
+ * AD runs as ONE kernel launch (256 threads) that reads and writes a
+ * per-thread host-mapped pinned staging buffer directly (no copies, one
+ * launch, completion seen by polling a done word the kernel writes last);
+ * larger ones stage through pinned memory and a device buffer.  Either way
+ * the tag is checked before plaintext is written, and every staging byte
+ * (key, AD, input, output) is zeroed before the call returns, also on error
+ * paths.  h_buf holds len plaintext bytes and has room for len+16 (encrypt),
+ * or holds ct_len = len+16 bytes (decrypt, plaintext written to
+ * h_buf[0..len) on success, h_buf untouched and NOISE_GPU_E_MAC returned on
+ * failure).  An all-zero key returns NOISE_GPU_E_ARG (rekey excepted). */
 int noise_gpu_encrypt_host(const uint8_t h_key[32], uint64_t nonce,
                            const uint8_t *h_ad, size_t ad_len, uint8_t *h_buf,
                            size_t len);
@@ -282,7 +299,10 @@ int noise_gpu_rekey_host(uint8_t h_key[32]);
  * (nkeys x 32 B), descriptors, h_in[0..in_bytes) and h_ad[0..ad_bytes) are
  * staged to the device, the records kernel runs, h_out[0..out_bytes) (and
  * h_status[nrec] for decrypt) are copied back.  Used by
- * CipherState::encrypt_batch / decrypt_batch. */
+ * CipherState::encrypt_batch / decrypt_batch.  Every descriptor range is
+ * bounds-checked against its buffer on the host (overflow-safe), and the
+ * device staging and the records scratch are zeroed before the call
+ * returns. */
 int noise_gpu_encrypt_records_host(const uint8_t *h_keys, uint32_t nkeys,
                                    const noise_gpu_record *h_recs,
                                    uint64_t nrec, const uint8_t *h_in,
@@ -300,7 +320,11 @@ int noise_gpu_decrypt_records_host(const uint8_t *h_keys, uint32_t nkeys,
  * double-buffered (H2D copy || kernel || D2H copy on separate streams).
  * Encrypt: h_in records of len bytes (stride in_stride) -> h_out records of
  * len+16 (stride out_stride).  Decrypt: the reverse, with h_status[nrec].
- * *seconds receives the wall time of the whole transfer-inclusive run. */
+ * *seconds receives the wall time of the whole call, from entry to return.
+ * Streams, events and device buffers live in a per-thread context that
+ * persists across calls (created on the first call, or when the calling
+ * thread's device changes); their contents are zeroed at the end of every
+ * call. */
 int noise_gpu_encrypt_uniform_host(const uint8_t h_key[32], uint64_t nonce0,
                                    const uint8_t *h_in, uint64_t in_stride,
                                    uint8_t *h_out, uint64_t out_stride,

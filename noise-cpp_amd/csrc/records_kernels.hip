@@ -772,6 +772,9 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   AuxStream ax;
   hipError_t e = aux_get(&ax, stream);
   if (e != hipSuccess) return e;
+#ifdef NOISE_RECORDS_SERIAL  // diagnostics only: every kernel on the caller's stream
+  ax.aux = stream;
+#endif
   const dim3 bt(64);
   const dim3 grid(capped((nrec + 63) / 64, NOISE_GRID_CAP));
   SegRec *rt = const_cast<SegRec *>(ta.rt);

@@ -6,7 +6,8 @@
 // The reference does one record per call on the CPU (noise.cpp:393-427 ->
 // monocypher.c:2899-2929).  Here one call = one kernel launch and no copy
 // engine: the workgroup pulls the staged AD and record straight over PCIe
-// into LDS (all pieces in flight at once), spreads the work over 256 lanes
+// into LDS (LDS-DMA, all pieces in flight at once, landing while the
+// keystream is computed), spreads the work over 256 lanes
 // and pushes the result back the same way, then raises a completion word in
 // the staging header that the host polls (no hipMemcpyAsync pair, no stream
 // synchronisation on the fast path).
@@ -81,16 +82,21 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_one(const OneArgs a) {
   // r, s, the verdict and 4 x 2 slots of per-wave Poly1305 sums
   const uint32_t s_tag = na + nl, s_r = s_tag + 1, s_s = s_r + 1, s_ok = s_s + 1, s_w = s_ok + 1;
 
-  // 1. staging -> LDS: AD, record and (decrypt) tag are contiguous pieces
+  // 1. staging -> LDS by LDS-DMA: AD, record and (decrypt) tag pieces land
+  // at lds[0..npc) without passing through registers, so nothing waits for
+  // the PCIe round trip until the keystream blocks below are computed
   {
     const uint32_t npc = na + nl + (DECRYPT ? 1u : 0u);
-    for (uint32_t i = t; i < npc; i += kOneBlock) {
-      const uint8_t *src = base + (i < na ? lay.ad + 16ull * i : lay.in + 16ull * (i - na));
-      const u32x4 v = *(const g_u32x4 *)src;
-      lds[i] = make_uint4(v.x, v.y, v.z, v.w);
+    // wave-uniform base (readfirstlane: M0 takes an SGPR)
+    for (uint32_t i0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(wave * 64u)); i0 < npc;
+         i0 += kOneBlock) {
+      const uint32_t i = i0 + lane;
+      if (i < npc) {
+        const uint8_t *src = base + (i < na ? lay.ad + 16ull * i : lay.in + 16ull * (i - na));
+        lds_dma16_v(src, (lds_void *)(lds + i0));
+      }
     }
   }
-  __syncthreads();
 
   // 2. keystream: block b on thread b % 256; block 0 = one-time Poly key
   const uint32_t nlo = (uint32_t)a.nonce, nhi = (uint32_t)(a.nonce >> 32);
@@ -101,6 +107,13 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_one(const OneArgs a) {
     const uint32_t b = t + (uint32_t)j * kOneBlock;
     if (b > nb) break;
     chacha20_block(a.key.w, b, nlo, nhi, ks[j]);
+  }
+  wait_vmem();  // this wave's DMA has landed ...
+  __syncthreads();  // ... and every other wave's
+#pragma unroll
+  for (int j = 0; j < kOneMaxKsPerThread; ++j) {
+    const uint32_t b = t + (uint32_t)j * kOneBlock;
+    if (b > nb) break;
     if (b == 0) {
       lds[s_r] = make_uint4(ks[j][0] & 0x0fffffffu, ks[j][1] & 0x0ffffffcu,
                             ks[j][2] & 0x0ffffffcu, ks[j][3] & 0x0ffffffcu);

@@ -20,8 +20,12 @@ RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set and
 exits with their status; rank 0 prints the JSON line.  Records shard per GPU
 with no data-path collective (cfg 2/3/4 weak scaling: each rank its own R
 records and nonce range; cfg 5 strong scaling: one 8 Mi-record range cut in
-contiguous slices).  torch.distributed (RCCL) carries only the barrier, the
-max-over-ranks of the elapsed time and the per-rank shard table.
+contiguous slices).  torch.distributed carries only the barrier, the
+max-over-ranks of the elapsed time and the per-rank shard table, over gloo
+(host TCP): with no data-path exchange there is nothing for RCCL to carry,
+and an initialised RCCL communicator slows every kernel on the GPU by 6-12 %
+(same-box A/B, tools/gpu/dist_ab.sh; profiles/round2/ab/ab_experiments.md).
+The barriers are bracketed by torch.cuda.synchronize() on both sides.
 
 --stub (tests only, CPU): the same launcher, rank bookkeeping, barriers and
 reductions over gloo, with a trivial host workload instead of the GPU.
@@ -69,6 +73,15 @@ def rank_nonce_base(cfg, rank, world, per_rank, total):
     if cfg == 5:
         return shard(total, rank, world)[0]
     return rank * per_rank
+
+
+def json_stdout():
+    """Keep the process's stdout for the one JSON line: point fd 1 at stderr
+    and return a writer on the original stdout."""
+    sys.stdout.flush()
+    fd = os.dup(1)
+    os.dup2(2, 1)
+    return os.fdopen(fd, "w")
 
 
 def reduce_over_ranks(dist, elapsed, nrec, device):
@@ -516,6 +529,12 @@ def parse(argv):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-config1", action="store_true",
                     help="skip the config-1 (XX loopback + 1000 x 1 KiB) leg of the N=1 line")
+    # test hook: initialise the process group (RCCL on GPUs) even at world
+    # size 1, so the barrier / reduction / gather path runs on a 1-GPU box
+    ap.add_argument("--force-dist", action="store_true", help=argparse.SUPPRESS)
+    # control-plane backend (tests / A/B only: gloo is the product choice)
+    ap.add_argument("--dist-backend", choices=("gloo", "nccl"), default="gloo",
+                    help=argparse.SUPPRESS)
     ap.add_argument("--host-inclusive", action="store_true",
                     help="also time the pinned-host H2D->kernel->D2H pipeline (DESIGN.md)")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
@@ -532,6 +551,9 @@ def main(argv=None):
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch(args, argv)
 
+    # the JSON line goes to the original stdout; everything else written to
+    # fd 1 from here on (library banners: RCCL, profilers) lands on stderr
+    out = json_stdout()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -541,7 +563,7 @@ def main(argv=None):
     if args.stub:
         import torch
         dev = "cpu"
-        if world > 1:
+        if world > 1 or args.force_dist:
             import torch.distributed as dist
             dist.init_process_group("gloo")
 
@@ -553,9 +575,12 @@ def main(argv=None):
         import torch
         torch.cuda.set_device(local)
         dev = "cuda"
-        if world > 1:
+        if world > 1 or args.force_dist:
             import torch.distributed as dist
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            if args.dist_backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group("gloo")
         noise_amd.load()
         stream = torch.cuda.current_stream()
         sync = torch.cuda.synchronize
@@ -596,7 +621,8 @@ def main(argv=None):
     elapsed = time.perf_counter() - t0
     shards = [{"rank": rank, "nonce_lo": wl["n_base"], "nonce_hi": wl["n_base"] + R, "records": R}]
     if dist:
-        elapsed, total_rec = reduce_over_ranks(dist, elapsed, R, dev)
+        red_dev = "cuda" if (dev == "cuda" and args.dist_backend == "nccl") else "cpu"
+        elapsed, total_rec = reduce_over_ranks(dist, elapsed, R, red_dev)
         gathered = [None] * world
         dist.all_gather_object(gathered, shards[0])
         shards = gathered
@@ -640,7 +666,8 @@ def main(argv=None):
     if rank == 0 and args.host_inclusive and cfg == 2 and not args.stub:
         line["host_inclusive"] = host_inclusive(R, L)
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        out.write(json.dumps(line) + "\n")
+        out.flush()
     if dist:
         dist.destroy_process_group()
     return 0

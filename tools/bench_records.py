@@ -49,7 +49,8 @@ def main():
         for _ in range(5):
             once()
         torch.cuda.synchronize()
-        assert int(d_st.sum()) == 0 and torch.equal(d_pt, d_back)
+        if not os.environ.get("NOISE_NO_CHECK"):  # ablation builds (timing only) skip it
+            assert int(d_st.sum()) == 0 and torch.equal(d_pt, d_back)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         reps, te, td = 10, 0.0, 0.0
         for _ in range(reps):

@@ -120,6 +120,35 @@ void hip_check(hipError_t e, const char *what) {
 }
 inline std::size_t align16(std::size_t x) { return (x + 15) & ~std::size_t(15); }
 inline std::size_t align256(std::size_t x) { return (x + 255) & ~std::size_t(255); }
+
+// Bulk message copy with streaming (non-temporal) stores.  A plain memcpy of
+// a 1 KiB message into a cold destination line first reads the line for
+// ownership, so every copied byte costs three memory transfers; streaming
+// stores write whole lines and skip that read.  The destination must be
+// 16-byte aligned (slot offsets are; so are the caller's result buffers in
+// the common case -- otherwise plain memcpy).  The caller issues
+// stream_fence() before anyone else (a DMA engine, another thread) reads.
+typedef std::uint32_t v4u32 __attribute__((ext_vector_type(4)));
+inline void stream_copy(std::uint8_t *dst, const std::uint8_t *src, std::size_t n) {
+  if (n < 256 || (reinterpret_cast<std::uintptr_t>(dst) & 15u) != 0) {
+    std::memcpy(dst, src, n);
+    return;
+  }
+  std::size_t i = 0;
+  for (; i + 64 <= n; i += 64) {
+    v4u32 a, b, c, d;
+    std::memcpy(&a, src + i, 16);
+    std::memcpy(&b, src + i + 16, 16);
+    std::memcpy(&c, src + i + 32, 16);
+    std::memcpy(&d, src + i + 48, 16);
+    __builtin_nontemporal_store(a, reinterpret_cast<v4u32 *>(dst + i));
+    __builtin_nontemporal_store(b, reinterpret_cast<v4u32 *>(dst + i + 16));
+    __builtin_nontemporal_store(c, reinterpret_cast<v4u32 *>(dst + i + 32));
+    __builtin_nontemporal_store(d, reinterpret_cast<v4u32 *>(dst + i + 48));
+  }
+  if (i < n) std::memcpy(dst + i, src + i, n - i);
+}
+inline void stream_fence() { __builtin_ia32_sfence(); }
 }  // namespace
 
 // Fork-join pool for the host byte copies (submit_batch / copy_out): the
@@ -350,7 +379,8 @@ std::size_t Pipeline::submit_batch(const Message *messages, std::size_t n) {
   pool_->run(k, [&](std::size_t lo, std::size_t hi) {
     for (std::size_t i = lo; i < hi; ++i)
       if (messages[i].len)
-        std::memcpy(sl.h + o_in_ + sl.recs()[base + i].in_off, messages[i].data, messages[i].len);
+        stream_copy(sl.h + o_in_ + sl.recs()[base + i].in_off, messages[i].data, messages[i].len);
+    stream_fence();  // visible to the H2D copy flush() issues
   });
   sl.nrec += k;
   sl.in_used = in_used;
@@ -360,7 +390,8 @@ std::size_t Pipeline::submit_batch(const Message *messages, std::size_t n) {
 
 void Pipeline::copy_out(const Batch &b, std::uint8_t *const *dst) {
   pool_->run(b.size(), [&](std::size_t lo, std::size_t hi) {
-    for (std::size_t i = lo; i < hi; ++i) std::memcpy(dst[i], b.data(i), b.length(i));
+    for (std::size_t i = lo; i < hi; ++i) stream_copy(dst[i], b.data(i), b.length(i));
+    stream_fence();
   });
 }
 

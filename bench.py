@@ -120,7 +120,7 @@ def launch(args, argv):
     if not args.stub:
         import torch
         have = torch.cuda.device_count()
-        if have < n:
+        if have < n and not args.share_device:
             raise SystemExit("bench.py --gpus %d: only %d GPU(s) visible" % (n, have))
     port = free_port()
     procs = []
@@ -538,6 +538,10 @@ def parse(argv):
     ap.add_argument("--host-inclusive", action="store_true",
                     help="also time the pinned-host H2D->kernel->D2H pipeline (DESIGN.md)")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
+    # test hook: ranks share the visible GPUs (rank r -> device r mod count),
+    # so the N-rank path runs end to end on a 1-GPU box (the rate is then
+    # not a scaling figure: the ranks split one GPU)
+    ap.add_argument("--share-device", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
 
@@ -573,6 +577,8 @@ def main(argv=None):
         wl = make_stub_workload(args, rank, world)
     else:
         import torch
+        if args.share_device:
+            local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
         dev = "cuda"
         if world > 1 or args.force_dist:
@@ -657,6 +663,8 @@ def main(argv=None):
                            **wl["config"]),
             "roofline": roofline(cfg, wl, enc_ms, dec_ms),
             "shards": shards}
+    if args.share_device:
+        line["note"] = "--share-device test run: the ranks split the visible GPU(s); not a scaling figure"
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.stub:
         log("cpu baseline ...")
         line["cpu_baseline"] = cpu_baseline()
@@ -686,10 +694,15 @@ def roofline(cfg, wl, enc_ms, dec_ms):
     achieved = kbytes / (kms * 1e-3)
     prof = latest_profile(cfg)
     pmc = pmc_kernels(prof, names)
+    # the profile's per-launch counts, scaled to this launch's records (a
+    # strong-scaling shard, or --records, launches fewer than were profiled)
+    scale = 1.0
+    if pmc and prof[1].get("records_per_launch"):
+        scale = wl["R"] / float(prof[1]["records_per_launch"])
     traffic = None
     if pmc and "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
         # gfx950: FETCH_SIZE reports half of a wide coalesced read stream
-        traffic = int((2.0 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024)
+        traffic = int((2.0 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024 * scale)
     roof = {"bound": "hbm", "kernel": names[0] if len(names) == 1 else
             "records call: " + ", ".join(n.replace("noise_amd::", "") + "*" for n in names),
             "direction": "decrypt" if d else "encrypt",
@@ -703,19 +716,21 @@ def roofline(cfg, wl, enc_ms, dec_ms):
             "avg_launch_ms": round(kms, 4), "enc_ms": round(enc_ms, 4), "dec_ms": round(dec_ms, 4),
             "pmc_source": prof[0] if prof else None,
             "binding_roof": "valu"}
+    if scale != 1.0:
+        roof["pmc_scaled"] = round(scale, 6)
     if pmc and "SQ_INSTS_VALU" in pmc:
-        vi = pmc["SQ_INSTS_VALU"]
+        vi = pmc["SQ_INSTS_VALU"] * scale
         valu = {"insts_per_launch": int(vi), "achieved": round(vi / (kms * 1e-3) / 1e9, 2),
                 "peak": round(VALU_PEAK / 1e9, 1), "unit": "G wave-instr/s",
                 "frac": round(vi / (kms * 1e-3) / VALU_PEAK, 4),
                 "issue_model": "1024 SIMDs x 2.4 GHz / 4 cycles per wave64 instruction (measured cost "
                                "of every instruction in a ChaCha/Poly1305 stream on gfx950)"}
         if "SQ_WAVES" in pmc and pmc["SQ_WAVES"]:
-            valu["insts_per_wave"] = int(vi / pmc["SQ_WAVES"])
+            valu["insts_per_wave"] = int(pmc["SQ_INSTS_VALU"] / pmc["SQ_WAVES"])
         if pmc.get("GRBM_GUI_ACTIVE"):
             # effective clock of the profiled dispatch (GRBM_GUI_ACTIVE sums 8 XCDs)
             busy = pmc["GRBM_GUI_ACTIVE"] / 8.0
-            valu["issue_util_profiled"] = round(vi * 4.0 / 1024.0 / busy, 4)
+            valu["issue_util_profiled"] = round(pmc["SQ_INSTS_VALU"] * 4.0 / 1024.0 / busy, 4)
         roof["valu"] = valu
     return roof
 

@@ -57,6 +57,9 @@ for f in ("bench_trace.json", "bench_pmc1.json"):
 json.dump({"source": "rocprofv3 --pmc, one counter group per pass (tools/gpu/profile_cfg.sh %d); "
                      "per-dispatch means" % cfg,
            "workload": bench_line["config"]["workload"] if bench_line else None,
+           # records per launch of the profiled run: bench.py scales the
+           # per-launch counts to its own shard size
+           "records_per_launch": bench_line["config"]["records_per_gpu"] if bench_line else None,
            "kernels": summary}, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
 traffic = {k: int((2.0 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024)
            for k, d in summary.items() if "FETCH_SIZE" in d and "WRITE_SIZE" in d}

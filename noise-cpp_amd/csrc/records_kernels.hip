@@ -101,7 +101,8 @@ struct RecHdr {
   unsigned long long cls_base[kCols];  // start of each class in idx
   unsigned long long nlong;            // long records handled as segments
   unsigned long long nseg;             // their full segments
-  unsigned long long pad[62 - 2 * kCols];
+  unsigned long long nfail;            // decrypt: long records whose tag failed
+  unsigned long long pad[61 - 2 * kCols];
 };
 static_assert(sizeof(RecHdr) == 512, "scratch header layout");
 
@@ -209,7 +210,10 @@ __global__ __launch_bounds__(64) void k_cls_scan(const uint32_t *part, uint32_t 
   if (lane == 63) {
     hdr->counts[c] = run;
     // lowered by k_cls_scatter if the segment scratch overflows
-    if (c == (uint32_t)kClsLong) hdr->nlong = run;
+    if (c == (uint32_t)kClsLong) {
+      hdr->nlong = run;
+      hdr->nfail = 0;
+    }
     if (c == (uint32_t)kColSegs) hdr->nseg = run < segcap ? run : segcap;
   }
 }
@@ -545,6 +549,129 @@ __global__ __launch_bounds__(64) void k_seg_finalize(
   }
 }
 
+// k_seg_finalize8: the same result with EIGHT lanes per long record (an
+// octet; a wave finalizes 8 records of similar segment count per pass), so a
+// 63-segment record is not one lane's chain of 63 dependent products and
+// load round trips.  Octet lane i takes segments i, i + 8, ... (at most 8,
+// loaded together) and runs Horner in R^8:
+//   acc_i = sum_k P_{i+8k} R^(8(K_i-1-k)),   K_i = ceil((nf - i) / 8)
+// then h = sum_i acc_i R^(e_i) with e_i = nf-1 - (i + 8(K_i-1)) in [0, 7]
+// (three selected products by R, R^2, R^4) and a 3-level xor butterfly over
+// the octet.  Octet lane 0 then appends the tail and writes / checks the tag
+// exactly as k_seg_finalize does.  Decrypt counts failed tags in hdr->nfail
+// so that k_seg_fixup can return at once when there are none.
+template <bool DECRYPT>
+__global__ __launch_bounds__(64) void k_seg_finalize8(
+    const uint32_t *__restrict__ fin, const SegRec *__restrict__ rt,
+    const SegPartial *__restrict__ partial, RecHdr *hdr, const uint8_t *in, uint8_t *out,
+    uint8_t *status) {
+  const uint64_t n = hdr->counts[kClsLong], nlong = hdr->nlong;
+  const uint32_t i = threadIdx.x & 7u;
+#pragma unroll 1
+  for (uint64_t base = (uint64_t)blockIdx.x * 8; base < n; base += (uint64_t)gridDim.x * 8) {
+    // every lane stays in the loop body (the butterfly reads all octet
+    // lanes); an octet without a record works on zeros and stores nothing
+    const uint64_t t = base + (threadIdx.x >> 3);
+    uint32_t q = t < n ? fin[t] : 0xffffffffu;
+    const bool ok = q < nlong;
+    if (!ok) q = 0;
+    uint32_t nf = 0;
+    uint64_t seg0 = 0;
+    F26 R1;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) R1.a[k] = k == 0 ? 1u : 0u;
+    if (ok) {
+      const SegRec &R = rt[q];
+      nf = R.nfull;
+      seg0 = R.seg0;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) R1.a[k] = R.r64[k];
+    }
+    // this lane's segments, all loads in flight together (nf <= 63: K <= 8)
+    const uint32_t K = nf > i ? (nf - i + 7u) >> 3 : 0u;
+    uint4 lo[8];
+    uint32_t hi[8];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+      lo[k] = make_uint4(0u, 0u, 0u, 0u);
+      hi[k] = 0u;
+      if (k < K) {
+        const SegPartial &P = partial[seg0 + i + 8u * k];
+        lo[k] = make_uint4(P.h[0], P.h[1], P.h[2], P.h[3]);
+        hi[k] = P.h[4];
+      }
+    }
+    const F26 R2 = mul26(R1, R1), R4 = mul26(R2, R2), R8 = mul26(R4, R4);
+    F26 acc = to26(lo[0].x, lo[0].y, lo[0].z, lo[0].w, hi[0]);  // zeros when K == 0
+#pragma unroll
+    for (uint32_t k = 1; k < 8; ++k) {
+      if (k < K) {
+        acc = mul26(acc, R8);
+        const F26 v = to26(lo[k].x, lo[k].y, lo[k].z, lo[k].w, hi[k]);
+#pragma unroll
+        for (int m = 0; m < 5; ++m) acc.a[m] += v.a[m];
+        carry26(acc);
+      }
+    }
+    // * R^(e_i): the lane's last segment is followed by e_i more
+    const uint32_t e = K ? nf - 1u - i - 8u * (K - 1u) : 0u;
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      const F26 &pw = b == 0 ? R1 : (b == 1 ? R2 : R4);
+      F26 f;
+      const bool use = (e >> b) & 1u;
+#pragma unroll
+      for (int m = 0; m < 5; ++m) f.a[m] = use ? pw.a[m] : (m == 0 ? 1u : 0u);
+      acc = mul26(acc, f);
+    }
+    // limbs < 2^26 + 2^9 after mul26: the octet's sum fits in 32 bits
+#pragma unroll
+    for (int b = 1; b < 8; b <<= 1) {
+#pragma unroll
+      for (int m = 0; m < 5; ++m) acc.a[m] += (uint32_t)__shfl_xor((int)acc.a[m], b);
+    }
+    if (i != 0 || !ok) continue;
+    const SegRec &R = rt[q];
+    const uint32_t len = R.len;
+    if (len & 1023u) {
+      carry26(acc);
+      F26 rtp;
+#pragma unroll
+      for (int m = 0; m < 5; ++m) rtp.a[m] = R.rtail[m];
+      acc = mul26(acc, rtp);
+      const F26 v = to26(R.ptail[0], R.ptail[1], R.ptail[2], R.ptail[3], R.ptail[4]);
+#pragma unroll
+      for (int m = 0; m < 5; ++m) acc.a[m] += v.a[m];
+    }
+    carry26(acc);
+    carry26(acc);
+    Poly1305 p;
+    from26(acc, p.h0, p.h1, p.h2, p.h3, p.h4);
+    p.r0 = R.r[0]; p.r1 = R.r[1]; p.r2 = R.r[2]; p.r3 = R.r[3];
+    p.rr0 = (p.r0 >> 2) * 5u;
+    p.rr1 = p.r1 + (p.r1 >> 2);
+    p.rr2 = p.r2 + (p.r2 >> 2);
+    p.rr3 = p.r3 + (p.r3 >> 2);
+    p.r0lo = p.r0 & 3u;
+    p.s0 = R.s[0]; p.s1 = R.s[1]; p.s2 = R.s[2]; p.s3 = R.s[3];
+    poly_block(p, 0u, 0u, len, 0u);  // LE64(ad_len = 0) || LE64(len)
+    uint32_t tag[4];
+    poly_final(p, tag);
+    if (!DECRYPT) {
+      uint8_t *tp = out + R.out_off + len;
+      if ((len & 15u) == 0) store16<true>(tp, make_uint4(tag[0], tag[1], tag[2], tag[3]), 16);
+      else store16<false>(tp, make_uint4(tag[0], tag[1], tag[2], tag[3]), 16);
+    } else {
+      const uint8_t *tp = in + R.in_off + len;
+      const uint4 want = (len & 15u) == 0 ? load16<true>(tp, 16) : load16<false>(tp, 16);
+      const uint32_t diff = (want.x ^ tag[0]) | (want.y ^ tag[1]) | (want.z ^ tag[2]) |
+                            (want.w ^ tag[3]);
+      status[R.di] = diff == 0u ? NOISE_GPU_REC_OK : NOISE_GPU_REC_BAD_MAC;
+      if (diff) atomicAdd(&hdr->nfail, 1ull);
+    }
+  }
+}
+
 // k_seg_fixup (decrypt): lane per full segment, then lane per tail.  The
 // segment and tail kernels wrote plaintext before the tag was known; for a
 // record whose tag failed, put the ciphertext back (in place: XOR the
@@ -554,6 +681,9 @@ __global__ __launch_bounds__(64) void k_seg_fixup(
     const SegEntry *__restrict__ segs, const uint32_t *__restrict__ tails,
     const SegRec *__restrict__ rt, const RecHdr *hdr, const uint8_t *in,
     uint8_t *out, const uint8_t *status) {
+#ifndef NOISE_FIN_LANE
+  if (hdr->nfail == 0) return;  // every long record verified (k_seg_finalize8)
+#endif
   const uint64_t nseg = hdr->nseg, ntail = hdr->counts[kColTails], nlong = hdr->nlong;
 #pragma unroll 1
   for (uint64_t g = (uint64_t)blockIdx.x * 64 + threadIdx.x; g < nseg + ntail;
@@ -808,8 +938,14 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   const dim3 gseg(capped((segbound + 63) / 64, NOISE_GRID_CAP));
   hipLaunchKernelGGL((k_aead_tile<DECRYPT, 1024, false, kTileSeg>), gseg, bt, 0, stream, a);
   if ((e = hipStreamWaitEvent(stream, ax.join, 0)) != hipSuccess) return e;
+#ifdef NOISE_FIN_LANE  // A/B: one lane per long record
   hipLaunchKernelGGL((k_seg_finalize<DECRYPT>), grid, bt, 0, stream, fin, ta.rt, ta.partial, hdr,
                      in, out, status);
+#else
+  const dim3 gfin(capped((nrec + 7) / 8, NOISE_GRID_CAP));
+  hipLaunchKernelGGL((k_seg_finalize8<DECRYPT>), gfin, bt, 0, stream, fin, ta.rt, ta.partial,
+                     const_cast<RecHdr *>(hdr), in, out, status);
+#endif
   if (DECRYPT) {
     const dim3 gfix(capped((segbound + nrec + 63) / 64, NOISE_GRID_CAP));
     hipLaunchKernelGGL(k_seg_fixup, gfix, bt, 0, stream, ta.segs, tails, ta.rt, hdr, in, out,

@@ -549,64 +549,72 @@ __global__ __launch_bounds__(64) void k_seg_finalize(
   }
 }
 
-// k_seg_finalize8: the same result with EIGHT lanes per long record (an
-// octet; a wave finalizes 8 records of similar segment count per pass), so a
+// k_seg_finalize_w: the same result with W lanes per long record (a group;
+// a wave finalizes 64 / W records of similar segment count per pass), so a
 // 63-segment record is not one lane's chain of 63 dependent products and
-// load round trips.  Octet lane i takes segments i, i + 8, ... (at most 8,
-// loaded together) and runs Horner in R^8:
-//   acc_i = sum_k P_{i+8k} R^(8(K_i-1-k)),   K_i = ceil((nf - i) / 8)
-// then h = sum_i acc_i R^(e_i) with e_i = nf-1 - (i + 8(K_i-1)) in [0, 7]
-// (three selected products by R, R^2, R^4) and a 3-level xor butterfly over
-// the octet.  Octet lane 0 then appends the tail and writes / checks the tag
-// exactly as k_seg_finalize does.  Decrypt counts failed tags in hdr->nfail
-// so that k_seg_fixup can return at once when there are none.
-template <bool DECRYPT>
-__global__ __launch_bounds__(64) void k_seg_finalize8(
+// load round trips.  Group lane i takes segments i, i + W, ... (loaded
+// together) and runs Horner in R^W:
+//   acc_i = sum_k P_{i+Wk} R^(W(K_i-1-k)),   K_i = ceil((nf - i) / W)
+// then h = sum_i acc_i R^(e_i) with e_i = nf-1 - (i + W(K_i-1)) in [0, W)
+// (log2 W selected products by R, R^2, ...) and a log2 W-level xor butterfly
+// over the group.  Group lane 0 then appends the tail and writes / checks the
+// tag exactly as k_seg_finalize does.  Every lane repeats the log2 W
+// squarings, so W trades chain length for redundant products: W = 4 keeps
+// the whole call cheaper than one lane per record (W = 8 is VALU-bound on
+// the squarings).  Decrypt counts failed tags in hdr->nfail so that
+// k_seg_fixup can return at once when there are none.
+template <bool DECRYPT, int W>
+__global__ __launch_bounds__(64) void k_seg_finalize_w(
     const uint32_t *__restrict__ fin, const SegRec *__restrict__ rt,
     const SegPartial *__restrict__ partial, RecHdr *hdr, const uint8_t *in, uint8_t *out,
     uint8_t *status) {
+  static_assert(W == 2 || W == 4 || W == 8, "lanes per record");
+  constexpr int LOGW = W == 2 ? 1 : (W == 4 ? 2 : 3);
+  constexpr uint32_t KMAX = (63u + W - 1u) / W;  // segments per lane (nf <= 63)
   const uint64_t n = hdr->counts[kClsLong], nlong = hdr->nlong;
-  const uint32_t i = threadIdx.x & 7u;
+  const uint32_t i = threadIdx.x & (W - 1u);
 #pragma unroll 1
-  for (uint64_t base = (uint64_t)blockIdx.x * 8; base < n; base += (uint64_t)gridDim.x * 8) {
-    // every lane stays in the loop body (the butterfly reads all octet
-    // lanes); an octet without a record works on zeros and stores nothing
-    const uint64_t t = base + (threadIdx.x >> 3);
+  for (uint64_t base = (uint64_t)blockIdx.x * (64 / W); base < n;
+       base += (uint64_t)gridDim.x * (64 / W)) {
+    // every lane stays in the loop body (the butterfly reads all group
+    // lanes); a group without a record works on zeros and stores nothing
+    const uint64_t t = base + (threadIdx.x / W);
     uint32_t q = t < n ? fin[t] : 0xffffffffu;
     const bool ok = q < nlong;
     if (!ok) q = 0;
     uint32_t nf = 0;
     uint64_t seg0 = 0;
-    F26 R1;
+    F26 pw[LOGW + 1];  // R^(2^b), b = 0 .. LOGW
 #pragma unroll
-    for (int k = 0; k < 5; ++k) R1.a[k] = k == 0 ? 1u : 0u;
+    for (int k = 0; k < 5; ++k) pw[0].a[k] = k == 0 ? 1u : 0u;
     if (ok) {
       const SegRec &R = rt[q];
       nf = R.nfull;
       seg0 = R.seg0;
 #pragma unroll
-      for (int k = 0; k < 5; ++k) R1.a[k] = R.r64[k];
+      for (int k = 0; k < 5; ++k) pw[0].a[k] = R.r64[k];
     }
-    // this lane's segments, all loads in flight together (nf <= 63: K <= 8)
-    const uint32_t K = nf > i ? (nf - i + 7u) >> 3 : 0u;
-    uint4 lo[8];
-    uint32_t hi[8];
+    // this lane's segments, all loads in flight together
+    const uint32_t K = nf > i ? (nf - i + W - 1u) / W : 0u;
+    uint4 lo[KMAX];
+    uint32_t hi[KMAX];
 #pragma unroll
-    for (uint32_t k = 0; k < 8; ++k) {
+    for (uint32_t k = 0; k < KMAX; ++k) {
       lo[k] = make_uint4(0u, 0u, 0u, 0u);
       hi[k] = 0u;
       if (k < K) {
-        const SegPartial &P = partial[seg0 + i + 8u * k];
+        const SegPartial &P = partial[seg0 + i + W * k];
         lo[k] = make_uint4(P.h[0], P.h[1], P.h[2], P.h[3]);
         hi[k] = P.h[4];
       }
     }
-    const F26 R2 = mul26(R1, R1), R4 = mul26(R2, R2), R8 = mul26(R4, R4);
+#pragma unroll
+    for (int b = 1; b <= LOGW; ++b) pw[b] = mul26(pw[b - 1], pw[b - 1]);
     F26 acc = to26(lo[0].x, lo[0].y, lo[0].z, lo[0].w, hi[0]);  // zeros when K == 0
 #pragma unroll
-    for (uint32_t k = 1; k < 8; ++k) {
+    for (uint32_t k = 1; k < KMAX; ++k) {
       if (k < K) {
-        acc = mul26(acc, R8);
+        acc = mul26(acc, pw[LOGW]);
         const F26 v = to26(lo[k].x, lo[k].y, lo[k].z, lo[k].w, hi[k]);
 #pragma unroll
         for (int m = 0; m < 5; ++m) acc.a[m] += v.a[m];
@@ -614,19 +622,18 @@ __global__ __launch_bounds__(64) void k_seg_finalize8(
       }
     }
     // * R^(e_i): the lane's last segment is followed by e_i more
-    const uint32_t e = K ? nf - 1u - i - 8u * (K - 1u) : 0u;
+    const uint32_t e = K ? nf - 1u - i - W * (K - 1u) : 0u;
 #pragma unroll
-    for (int b = 0; b < 3; ++b) {
-      const F26 &pw = b == 0 ? R1 : (b == 1 ? R2 : R4);
+    for (int b = 0; b < LOGW; ++b) {
       F26 f;
       const bool use = (e >> b) & 1u;
 #pragma unroll
-      for (int m = 0; m < 5; ++m) f.a[m] = use ? pw.a[m] : (m == 0 ? 1u : 0u);
+      for (int m = 0; m < 5; ++m) f.a[m] = use ? pw[b].a[m] : (m == 0 ? 1u : 0u);
       acc = mul26(acc, f);
     }
-    // limbs < 2^26 + 2^9 after mul26: the octet's sum fits in 32 bits
+    // limbs < 2^26 + 2^9 after mul26: the group's sum fits in 32 bits
 #pragma unroll
-    for (int b = 1; b < 8; b <<= 1) {
+    for (int b = 1; b < W; b <<= 1) {
 #pragma unroll
       for (int m = 0; m < 5; ++m) acc.a[m] += (uint32_t)__shfl_xor((int)acc.a[m], b);
     }
@@ -682,7 +689,7 @@ __global__ __launch_bounds__(64) void k_seg_fixup(
     const SegRec *__restrict__ rt, const RecHdr *hdr, const uint8_t *in,
     uint8_t *out, const uint8_t *status) {
 #ifndef NOISE_FIN_LANE
-  if (hdr->nfail == 0) return;  // every long record verified (k_seg_finalize8)
+  if (hdr->nfail == 0) return;  // every long record verified (k_seg_finalize_w)
 #endif
   const uint64_t nseg = hdr->nseg, ntail = hdr->counts[kColTails], nlong = hdr->nlong;
 #pragma unroll 1
@@ -942,9 +949,12 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   hipLaunchKernelGGL((k_seg_finalize<DECRYPT>), grid, bt, 0, stream, fin, ta.rt, ta.partial, hdr,
                      in, out, status);
 #else
-  const dim3 gfin(capped((nrec + 7) / 8, NOISE_GRID_CAP));
-  hipLaunchKernelGGL((k_seg_finalize8<DECRYPT>), gfin, bt, 0, stream, fin, ta.rt, ta.partial,
-                     const_cast<RecHdr *>(hdr), in, out, status);
+#ifndef NOISE_FIN_W
+#define NOISE_FIN_W 4
+#endif
+  const dim3 gfin(capped((nrec + 64 / NOISE_FIN_W - 1) / (64 / NOISE_FIN_W), NOISE_GRID_CAP));
+  hipLaunchKernelGGL((k_seg_finalize_w<DECRYPT, NOISE_FIN_W>), gfin, bt, 0, stream, fin, ta.rt,
+                     ta.partial, const_cast<RecHdr *>(hdr), in, out, status);
 #endif
   if (DECRYPT) {
     const dim3 gfix(capped((segbound + nrec + 63) / 64, NOISE_GRID_CAP));

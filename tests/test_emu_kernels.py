@@ -17,11 +17,12 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EMU = os.path.join(ROOT, "tools", "emu")
+JOBS = "-j%d" % max(1, min(8, os.cpu_count() or 1))  # the ASan objects build in parallel
 BIN = os.path.join(EMU, "build", "emu_records")
 
 
 def _build(*extra):
-    r = subprocess.run(["make", "-C", EMU, "GRID_CAP=3u", *extra], capture_output=True,
+    r = subprocess.run(["make", JOBS, "-C", EMU, "GRID_CAP=3u", *extra], capture_output=True,
                        text=True, timeout=900)
     if r.returncode != 0:
         pytest.fail("emulation build failed:\n" + r.stdout[-2000:] + r.stderr[-4000:])
@@ -63,7 +64,7 @@ def test_host_entry_points_emulated_and_wiped():
     AddressSanitizer, bit-exact against the oracle, and after EVERY call every
     buffer the engine allocated is zero: no key, plaintext, ciphertext or
     one-time key is left in staging or scratch (monocypher.c:163-167)."""
-    r = subprocess.run(["make", "-C", EMU, "GRID_CAP=3u", "api"], capture_output=True, text=True,
+    r = subprocess.run(["make", JOBS, "-C", EMU, "GRID_CAP=3u", "api"], capture_output=True, text=True,
                        timeout=900)
     if r.returncode != 0:
         pytest.fail("emulation build failed:\n" + r.stdout[-2000:] + r.stderr[-4000:])
@@ -86,7 +87,7 @@ def test_emulated_batched_handshakes():
     host driver (csrc/handshake_batch.hip), unmodified, on the CPU under ASan:
     the reference's 110 vectors through noise_gpu_hs_* -- messages, handshake
     hashes, split keys, transport records under them vs the oracle."""
-    r = subprocess.run(["make", "-C", EMU, "handshake"], capture_output=True, text=True, timeout=900)
+    r = subprocess.run(["make", JOBS, "-C", EMU, "handshake"], capture_output=True, text=True, timeout=900)
     if r.returncode != 0:
         pytest.fail("emulation build failed:\n" + r.stdout[-2000:] + r.stderr[-4000:])
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
@@ -101,7 +102,7 @@ def test_emulated_fixed_base_public_keys():
     """x25519_device.hpp's fixed-base path (edwards25519 radix-16 table,
     constant-time selects) on the CPU under ASan: RFC 7748 §6.1 and random /
     extreme scalars against the device ladder with u = 9 and the host X25519."""
-    r = subprocess.run(["make", "-C", EMU, "handshake"], capture_output=True, text=True, timeout=900)
+    r = subprocess.run(["make", JOBS, "-C", EMU, "handshake"], capture_output=True, text=True, timeout=900)
     if r.returncode != 0:
         pytest.fail("emulation build failed:\n" + r.stdout[-2000:] + r.stderr[-4000:])
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")

@@ -321,10 +321,11 @@ int noise_gpu_decrypt_records_host(const uint8_t *h_keys, uint32_t nkeys,
  * Encrypt: h_in records of len bytes (stride in_stride) -> h_out records of
  * len+16 (stride out_stride).  Decrypt: the reverse, with h_status[nrec].
  * *seconds receives the wall time of the whole call, from entry to return.
- * Streams, events and device buffers live in a per-thread context that
- * persists across calls (created on the first call, or when the calling
- * thread's device changes); their contents are zeroed at the end of every
- * call. */
+ * Streams, events and device buffers live in a context per (calling thread,
+ * current device) that persists across calls (created on the thread's first
+ * call on that device; a thread serving several GPUs keeps one per device);
+ * their contents are zeroed at the end of every call.  The single-record
+ * and descriptor host entry points above keep their staging the same way. */
 int noise_gpu_encrypt_uniform_host(const uint8_t h_key[32], uint64_t nonce0,
                                    const uint8_t *h_in, uint64_t in_stride,
                                    uint8_t *h_out, uint64_t out_stride,

@@ -126,7 +126,23 @@ struct Staging {
     return NOISE_GPU_OK;
   }
 };
-thread_local Staging g_stage;
+// Contexts are kept per (thread, device): a thread that serves several GPUs
+// (hipSetDevice between calls) keeps every device's streams and buffers
+// instead of freeing and re-creating them on each switch.  Devices beyond
+// kMaxCtxDev share slots, whose reserve() re-targets on a switch.
+constexpr int kMaxCtxDev = 16;
+template <class Ctx>
+static Ctx *ctx_of(Ctx (&tab)[kMaxCtxDev]) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return nullptr;
+  return &tab[dev % kMaxCtxDev];
+}
+thread_local Staging g_stage_tab[kMaxCtxDev];
+// the calling thread's staging on its current device (nullptr: no device)
+#define NOISE_STAGE(var)                                                       \
+  Staging *var##_p = ctx_of(g_stage_tab);                                      \
+  if (!var##_p) return hip_fail(hipErrorInvalidDevice, "hipGetDevice");             \
+  Staging &var = *var##_p
 
 // Per-thread latency-path context (single_kernels.hip): a stream and a
 // host-mapped, coherent pinned staging image the kernel reads and writes
@@ -187,7 +203,7 @@ struct OneCtx {
     }
   }
 };
-thread_local OneCtx g_one;
+thread_local OneCtx g_one_tab[kMaxCtxDev];
 
 // One record through the latency kernel.  dec: in = ct (len bytes) + tag.
 // Returns the kernel's status in *st (decrypt); out receives len (+16 on
@@ -195,9 +211,11 @@ thread_local OneCtx g_one;
 int one_record(bool dec, const uint8_t key[32], uint64_t nonce, const uint8_t *ad, uint32_t ad_len,
                const uint8_t *in, uint32_t len, const uint8_t *tag, uint8_t *out, uint32_t *st) {
   const noise_amd::OneLayout lay = noise_amd::one_layout(ad_len, len);
-  int rc = g_one.reserve(lay.total);
+  OneCtx *cp = ctx_of(g_one_tab);
+  if (!cp) return hip_fail(hipErrorInvalidDevice, "hipGetDevice");
+  int rc = cp->reserve(lay.total);
   if (rc) return rc;
-  OneCtx &c = g_one;
+  OneCtx &c = *cp;
   if (ad_len) std::memcpy(c.h + lay.ad, ad, ad_len);
   if (len) std::memcpy(c.h + lay.in, in, len);
   if (dec) std::memcpy(c.h + lay.tag, tag, 16);
@@ -442,8 +460,8 @@ int noise_gpu_encrypt_host(const uint8_t h_key[32], uint64_t nonce,
                       h_buf, nullptr);
   // large AD or record: copy-staged through device scratch, the lane walk
   const size_t ad_sz = align16(ad_len), rec_sz = align16(len + 16);
-  if ((rc = g_stage.reserve(ad_sz + rec_sz))) return rc;
-  Staging &s = g_stage;
+  NOISE_STAGE(s);
+  if ((rc = s.reserve(ad_sz + rec_sz))) return rc;
   std::memcpy(s.h, h_ad, ad_len);
   std::memcpy(s.h + ad_sz, h_buf, len);
   uint32_t k[8];
@@ -482,8 +500,8 @@ int noise_gpu_decrypt_host(const uint8_t h_key[32], uint64_t nonce,
                     h_buf + len, h_buf, &st);
   } else {  // large AD or record: copy-staged through device scratch, the lane walk
     const size_t ad_sz = align16(ad_len), in_sz = align16(ct_len), out_sz = align16(len);
-    if ((rc = g_stage.reserve(ad_sz + in_sz + out_sz + 16))) return rc;
-    Staging &s = g_stage;
+    NOISE_STAGE(s);
+    if ((rc = s.reserve(ad_sz + in_sz + out_sz + 16))) return rc;
     uint8_t *d_in = s.d + ad_sz, *d_out = d_in + in_sz, *d_st = d_out + out_sz;
     std::memcpy(s.h, h_ad, ad_len);
     std::memcpy(s.h + ad_sz, h_buf, ct_len);
@@ -551,8 +569,8 @@ static int records_host(bool decrypt, const uint8_t *h_keys, uint32_t nkeys,
                o_in = o_recs + align16(sizeof(noise_gpu_record) * nrec),
                o_out = o_in + align16(in_bytes), o_ad = o_out + align16(out_bytes),
                o_st = o_ad + align16(ad_bytes), total = o_st + align16(nrec);
-  if ((rc = g_stage.reserve(total))) return rc;
-  Staging &s = g_stage;
+  NOISE_STAGE(s);
+  if ((rc = s.reserve(total))) return rc;
   std::memcpy(s.h + o_keys, h_keys, 32ull * nkeys);
   std::memcpy(s.h + o_recs, h_recs, sizeof(noise_gpu_record) * nrec);
   if (in_bytes) std::memcpy(s.h + o_in, h_in, in_bytes);
@@ -635,7 +653,7 @@ struct PipeCtx {
     return NOISE_GPU_OK;
   }
 };
-thread_local PipeCtx g_pipe;
+thread_local PipeCtx g_pipe_tab[kMaxCtxDev];
 }  // namespace
 
 static int uniform_host(bool decrypt, const uint8_t h_key[32], uint64_t nonce0,
@@ -655,8 +673,10 @@ static int uniform_host(bool decrypt, const uint8_t h_key[32], uint64_t nonce0,
     return NOISE_GPU_OK;
   }
   if ((rc = check_device())) return rc;
-  if ((rc = g_pipe.ready())) return rc;
-  PipeCtx &P = g_pipe;
+  PipeCtx *pp = ctx_of(g_pipe_tab);
+  if (!pp) return hip_fail(hipErrorInvalidDevice, "hipGetDevice");
+  if ((rc = pp->ready())) return rc;
+  PipeCtx &P = *pp;
   const uint64_t in_rec = decrypt ? (uint64_t)len + 16 : len;
   const uint64_t out_rec = decrypt ? len : (uint64_t)len + 16;
   // device chunks are packed (stride = record size), ~32 MiB of in + out
@@ -691,7 +711,7 @@ static int uniform_host(bool decrypt, const uint8_t h_key[32], uint64_t nonce0,
   for (int i = 0; i < PipeCtx::kDepth; ++i)
     if (used[i]) (void)hipMemsetAsync(P.buf[i], 0, used[i], P.st[i]);
   if (e != hipSuccess) {
-    g_pipe.release();
+    P.release();
     return hip_fail(e, "host pipeline");
   }
   if (seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();

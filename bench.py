@@ -408,8 +408,10 @@ def make_workload(cfg, args, rank, world, stream):
     elif cfg == 4:
         R = args.records or (1 << 20)
         lens = zipf_lengths(R)
-        in_sz = (lens + np.uint64(15)) // np.uint64(16) * np.uint64(16)
-        ct_sz = (lens + np.uint64(31)) // np.uint64(16) * np.uint64(16)
+        # records packed at 16-byte alignment (--rec-align: a layout study)
+        al = np.uint64(args.rec_align)
+        in_sz = (lens + al - np.uint64(1)) // al * al
+        ct_sz = (lens + np.uint64(16) + al - np.uint64(1)) // al * al
         in_off = np.concatenate([[0], np.cumsum(in_sz)[:-1]]).astype(np.uint64)
         ct_off = np.concatenate([[0], np.cumsum(ct_sz)[:-1]]).astype(np.uint64)
         n_base = rank * R
@@ -538,6 +540,8 @@ def parse(argv):
     ap.add_argument("--host-inclusive", action="store_true",
                     help="also time the pinned-host H2D->kernel->D2H pipeline (DESIGN.md)")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
+    # layout study (config 4): byte alignment of each record's offsets
+    ap.add_argument("--rec-align", type=int, default=16, help=argparse.SUPPRESS)
     # test hook: ranks share the visible GPUs (rank r -> device r mod count),
     # so the N-rank path runs end to end on a 1-GPU box (the rate is then
     # not a scaling figure: the ranks split one GPU)

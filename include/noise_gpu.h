@@ -337,6 +337,48 @@ int noise_gpu_decrypt_uniform_host(const uint8_t h_key[32], uint64_t nonce0,
                                    uint32_t len, uint8_t *h_status,
                                    uint64_t nrec, double *seconds);
 
+/* ---- explicit device contexts --------------------------------------------
+ * SURVEY 8(b) proposed noise_gpu_ctx_create(int device, ...).  The device-
+ * resident entry points above need no context (a stream names the device's
+ * work; the records scratch is kept per (device, stream)).  The host-buffer
+ * entry points otherwise keep their staging per (calling thread, current
+ * device); a noise_gpu_ctx instead owns that state for one device, so a
+ * server can bind one context per GPU (or per connection thread) without
+ * relying on hipSetDevice state.  Each noise_gpu_ctx_* call makes the
+ * context's device current for its duration and restores the caller's
+ * device afterwards; it behaves exactly like the context-free function of
+ * the same name.  A context is not thread-safe: one thread at a time (like
+ * a CipherState).  destroy wipes and frees everything the context staged. */
+typedef struct noise_gpu_ctx noise_gpu_ctx;
+/* device: HIP device index (must be gfx950, else NOISE_GPU_E_NODEV) */
+int noise_gpu_ctx_create(int device, noise_gpu_ctx **out);
+int noise_gpu_ctx_destroy(noise_gpu_ctx *ctx);
+int noise_gpu_ctx_device(const noise_gpu_ctx *ctx, int *device);
+int noise_gpu_ctx_encrypt_host(noise_gpu_ctx *ctx, const uint8_t h_key[32], uint64_t nonce,
+                               const uint8_t *h_ad, size_t ad_len, uint8_t *h_buf, size_t len);
+int noise_gpu_ctx_decrypt_host(noise_gpu_ctx *ctx, const uint8_t h_key[32], uint64_t nonce,
+                               const uint8_t *h_ad, size_t ad_len, uint8_t *h_buf,
+                               size_t ct_len);
+int noise_gpu_ctx_rekey_host(noise_gpu_ctx *ctx, uint8_t h_key[32]);
+int noise_gpu_ctx_encrypt_records_host(noise_gpu_ctx *ctx, const uint8_t *h_keys, uint32_t nkeys,
+                                       const noise_gpu_record *h_recs, uint64_t nrec,
+                                       const uint8_t *h_in, uint64_t in_bytes, uint8_t *h_out,
+                                       uint64_t out_bytes, const uint8_t *h_ad,
+                                       uint64_t ad_bytes);
+int noise_gpu_ctx_decrypt_records_host(noise_gpu_ctx *ctx, const uint8_t *h_keys, uint32_t nkeys,
+                                       const noise_gpu_record *h_recs, uint64_t nrec,
+                                       const uint8_t *h_in, uint64_t in_bytes, uint8_t *h_out,
+                                       uint64_t out_bytes, const uint8_t *h_ad,
+                                       uint64_t ad_bytes, uint8_t *h_status);
+int noise_gpu_ctx_encrypt_uniform_host(noise_gpu_ctx *ctx, const uint8_t h_key[32],
+                                       uint64_t nonce0, const uint8_t *h_in, uint64_t in_stride,
+                                       uint8_t *h_out, uint64_t out_stride, uint32_t len,
+                                       uint64_t nrec, double *seconds);
+int noise_gpu_ctx_decrypt_uniform_host(noise_gpu_ctx *ctx, const uint8_t h_key[32],
+                                       uint64_t nonce0, const uint8_t *h_in, uint64_t in_stride,
+                                       uint8_t *h_out, uint64_t out_stride, uint32_t len,
+                                       uint8_t *h_status, uint64_t nrec, double *seconds);
+
 /* ---- synthetic data (bench / tests) ------------------------------------
  * Fill d_dst[0..nbytes) with the splitmix64 stream: byte j = byte (j & 7)
  * of mix64(seed + ((offset+j)/8 + 1) * 0x9e3779b97f4a7c15), offset-relative

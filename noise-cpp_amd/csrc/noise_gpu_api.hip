@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <new>
 #include <string>
 
 #include "launchers.hpp"
@@ -138,9 +139,12 @@ static Ctx *ctx_of(Ctx (&tab)[kMaxCtxDev]) {
   return &tab[dev % kMaxCtxDev];
 }
 thread_local Staging g_stage_tab[kMaxCtxDev];
+// An explicit noise_gpu_ctx (noise_gpu_ctx_* entry points) substitutes its
+// own contexts for the thread's for the duration of one call.
+thread_local Staging *tl_stage = nullptr;
 // the calling thread's staging on its current device (nullptr: no device)
 #define NOISE_STAGE(var)                                                       \
-  Staging *var##_p = ctx_of(g_stage_tab);                                      \
+  Staging *var##_p = tl_stage ? tl_stage : ctx_of(g_stage_tab);                \
   if (!var##_p) return hip_fail(hipErrorInvalidDevice, "hipGetDevice");             \
   Staging &var = *var##_p
 
@@ -204,6 +208,7 @@ struct OneCtx {
   }
 };
 thread_local OneCtx g_one_tab[kMaxCtxDev];
+thread_local OneCtx *tl_one = nullptr;
 
 // One record through the latency kernel.  dec: in = ct (len bytes) + tag.
 // Returns the kernel's status in *st (decrypt); out receives len (+16 on
@@ -211,7 +216,7 @@ thread_local OneCtx g_one_tab[kMaxCtxDev];
 int one_record(bool dec, const uint8_t key[32], uint64_t nonce, const uint8_t *ad, uint32_t ad_len,
                const uint8_t *in, uint32_t len, const uint8_t *tag, uint8_t *out, uint32_t *st) {
   const noise_amd::OneLayout lay = noise_amd::one_layout(ad_len, len);
-  OneCtx *cp = ctx_of(g_one_tab);
+  OneCtx *cp = tl_one ? tl_one : ctx_of(g_one_tab);
   if (!cp) return hip_fail(hipErrorInvalidDevice, "hipGetDevice");
   int rc = cp->reserve(lay.total);
   if (rc) return rc;
@@ -654,6 +659,7 @@ struct PipeCtx {
   }
 };
 thread_local PipeCtx g_pipe_tab[kMaxCtxDev];
+thread_local PipeCtx *tl_pipe = nullptr;
 }  // namespace
 
 static int uniform_host(bool decrypt, const uint8_t h_key[32], uint64_t nonce0,
@@ -673,7 +679,7 @@ static int uniform_host(bool decrypt, const uint8_t h_key[32], uint64_t nonce0,
     return NOISE_GPU_OK;
   }
   if ((rc = check_device())) return rc;
-  PipeCtx *pp = ctx_of(g_pipe_tab);
+  PipeCtx *pp = tl_pipe ? tl_pipe : ctx_of(g_pipe_tab);
   if (!pp) return hip_fail(hipErrorInvalidDevice, "hipGetDevice");
   if ((rc = pp->ready())) return rc;
   PipeCtx &P = *pp;
@@ -736,4 +742,142 @@ int noise_gpu_decrypt_uniform_host(const uint8_t h_key[32], uint64_t nonce0,
                       len, h_status, nrec, seconds);
 }
 
+
+// ---- explicit device contexts -------------------------------------------
+// A noise_gpu_ctx owns the host-entry-point contexts (staging, latency
+// path, pipeline) of one device.  Its entry points make that device current
+// and the ctx's contexts the thread's for the duration of the call, then
+// restore both.
+}  // extern "C"
+
+struct noise_gpu_ctx {
+  int device = -1;
+  Staging stage;
+  OneCtx one;
+  PipeCtx pipe;
+};
+
+namespace {
+struct CtxScope {
+  int prev = -1;
+  Staging *s0;
+  OneCtx *o0;
+  PipeCtx *p0;
+  int rc = NOISE_GPU_OK;
+  explicit CtxScope(noise_gpu_ctx *c) : s0(tl_stage), o0(tl_one), p0(tl_pipe) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    const hipError_t e = hipSetDevice(c->device);
+    if (e != hipSuccess) {
+      rc = hip_fail(e, "hipSetDevice(ctx device)");
+      return;
+    }
+    tl_stage = &c->stage;
+    tl_one = &c->one;
+    tl_pipe = &c->pipe;
+  }
+  ~CtxScope() {
+    tl_stage = s0;
+    tl_one = o0;
+    tl_pipe = p0;
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+}  // namespace
+
+#define NOISE_CTX_CALL(ctx, call)                                              \
+  do {                                                                         \
+    if (!(ctx)) return arg_fail("null context");                               \
+    CtxScope scope_(ctx);                                                      \
+    if (scope_.rc) return scope_.rc;                                           \
+    return call;                                                               \
+  } while (0)
+
+extern "C" {
+
+int noise_gpu_ctx_create(int device, noise_gpu_ctx **out) {
+  if (!out) return arg_fail("null output pointer");
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+    g_last_error = "no HIP device visible";
+    return NOISE_GPU_E_NODEV;
+  }
+  if (device < 0 || device >= n) return arg_fail("device index out of range");
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  HIP_TRY(hipSetDevice(device));
+  const int rc = check_device();  // gfx950 only
+  if (prev >= 0) (void)hipSetDevice(prev);
+  if (rc) return rc;
+  noise_gpu_ctx *c = new (std::nothrow) noise_gpu_ctx;
+  if (!c) return arg_fail("out of host memory");
+  c->device = device;
+  *out = c;
+  return NOISE_GPU_OK;
+}
+
+int noise_gpu_ctx_destroy(noise_gpu_ctx *ctx) {
+  if (!ctx) return NOISE_GPU_OK;
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  (void)hipSetDevice(ctx->device);
+  delete ctx;  // the contexts wipe what they staged, then free it
+  if (prev >= 0) (void)hipSetDevice(prev);
+  return NOISE_GPU_OK;
+}
+
+int noise_gpu_ctx_device(const noise_gpu_ctx *ctx, int *device) {
+  if (!ctx || !device) return arg_fail("null argument");
+  *device = ctx->device;
+  return NOISE_GPU_OK;
+}
+
+int noise_gpu_ctx_encrypt_host(noise_gpu_ctx *ctx, const uint8_t h_key[32], uint64_t nonce,
+                               const uint8_t *h_ad, size_t ad_len, uint8_t *h_buf, size_t len) {
+  NOISE_CTX_CALL(ctx, noise_gpu_encrypt_host(h_key, nonce, h_ad, ad_len, h_buf, len));
+}
+
+int noise_gpu_ctx_decrypt_host(noise_gpu_ctx *ctx, const uint8_t h_key[32], uint64_t nonce,
+                               const uint8_t *h_ad, size_t ad_len, uint8_t *h_buf,
+                               size_t ct_len) {
+  NOISE_CTX_CALL(ctx, noise_gpu_decrypt_host(h_key, nonce, h_ad, ad_len, h_buf, ct_len));
+}
+
+int noise_gpu_ctx_rekey_host(noise_gpu_ctx *ctx, uint8_t h_key[32]) {
+  NOISE_CTX_CALL(ctx, noise_gpu_rekey_host(h_key));
+}
+
+int noise_gpu_ctx_encrypt_records_host(noise_gpu_ctx *ctx, const uint8_t *h_keys, uint32_t nkeys,
+                                       const noise_gpu_record *h_recs, uint64_t nrec,
+                                       const uint8_t *h_in, uint64_t in_bytes, uint8_t *h_out,
+                                       uint64_t out_bytes, const uint8_t *h_ad,
+                                       uint64_t ad_bytes) {
+  NOISE_CTX_CALL(ctx, noise_gpu_encrypt_records_host(h_keys, nkeys, h_recs, nrec, h_in, in_bytes,
+                                                     h_out, out_bytes, h_ad, ad_bytes));
+}
+
+int noise_gpu_ctx_decrypt_records_host(noise_gpu_ctx *ctx, const uint8_t *h_keys, uint32_t nkeys,
+                                       const noise_gpu_record *h_recs, uint64_t nrec,
+                                       const uint8_t *h_in, uint64_t in_bytes, uint8_t *h_out,
+                                       uint64_t out_bytes, const uint8_t *h_ad,
+                                       uint64_t ad_bytes, uint8_t *h_status) {
+  NOISE_CTX_CALL(ctx, noise_gpu_decrypt_records_host(h_keys, nkeys, h_recs, nrec, h_in, in_bytes,
+                                                     h_out, out_bytes, h_ad, ad_bytes, h_status));
+}
+
+int noise_gpu_ctx_encrypt_uniform_host(noise_gpu_ctx *ctx, const uint8_t h_key[32],
+                                       uint64_t nonce0, const uint8_t *h_in, uint64_t in_stride,
+                                       uint8_t *h_out, uint64_t out_stride, uint32_t len,
+                                       uint64_t nrec, double *seconds) {
+  NOISE_CTX_CALL(ctx, uniform_host(false, h_key, nonce0, h_in, in_stride, h_out, out_stride, len,
+                                   nullptr, nrec, seconds));
+}
+
+int noise_gpu_ctx_decrypt_uniform_host(noise_gpu_ctx *ctx, const uint8_t h_key[32],
+                                       uint64_t nonce0, const uint8_t *h_in, uint64_t in_stride,
+                                       uint8_t *h_out, uint64_t out_stride, uint32_t len,
+                                       uint8_t *h_status, uint64_t nrec, double *seconds) {
+  NOISE_CTX_CALL(ctx, uniform_host(true, h_key, nonce0, h_in, in_stride, h_out, out_stride, len,
+                                   h_status, nrec, seconds));
+}
 }  // extern "C"

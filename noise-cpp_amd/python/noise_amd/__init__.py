@@ -117,6 +117,24 @@ def load(path=LIB_PATH):
         "noise_gpu_decrypt_uniform_host": (ctypes.c_int, [ctypes.c_char_p, u64, u8p, u64, u8p, u64,
                                                           u32, u8p, u64,
                                                           ctypes.POINTER(ctypes.c_double)]),
+        "noise_gpu_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+        "noise_gpu_ctx_destroy": (ctypes.c_int, [vp]),
+        "noise_gpu_ctx_device": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int)]),
+        "noise_gpu_ctx_encrypt_host": (ctypes.c_int, [vp, ctypes.c_char_p, u64, u8p, ctypes.c_size_t,
+                                                      u8p, ctypes.c_size_t]),
+        "noise_gpu_ctx_decrypt_host": (ctypes.c_int, [vp, ctypes.c_char_p, u64, u8p, ctypes.c_size_t,
+                                                      u8p, ctypes.c_size_t]),
+        "noise_gpu_ctx_rekey_host": (ctypes.c_int, [vp, u8p]),
+        "noise_gpu_ctx_encrypt_records_host": (ctypes.c_int, [vp, u8p, u32, u8p, u64, u8p, u64, u8p,
+                                                              u64, u8p, u64]),
+        "noise_gpu_ctx_decrypt_records_host": (ctypes.c_int, [vp, u8p, u32, u8p, u64, u8p, u64, u8p,
+                                                              u64, u8p, u64, u8p]),
+        "noise_gpu_ctx_encrypt_uniform_host": (ctypes.c_int, [vp, ctypes.c_char_p, u64, u8p, u64, u8p,
+                                                              u64, u32, u64,
+                                                              ctypes.POINTER(ctypes.c_double)]),
+        "noise_gpu_ctx_decrypt_uniform_host": (ctypes.c_int, [vp, ctypes.c_char_p, u64, u8p, u64, u8p,
+                                                              u64, u32, u8p, u64,
+                                                              ctypes.POINTER(ctypes.c_double)]),
         "noise_gpu_fill_synthetic": (ctypes.c_int, [u8p, u64, u64, u64, vp]),
         "noise_gpu_scratch_wipe": (ctypes.c_int, [vp]),
         "noise_gpu_hs_create": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, u64,

@@ -92,6 +92,18 @@ def test_no_device_fails_loudly():
     assert lib.noise_gpu_rekey_host(ctypes.create_string_buffer(32)) == noise_amd.E_NODEV
 
 
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a GPU is visible")
+def test_context_api_without_device():
+    lib = noise_amd.load()
+    h = ctypes.c_void_p()
+    assert lib.noise_gpu_ctx_create(0, ctypes.byref(h)) == noise_amd.E_NODEV and not h.value
+    assert lib.noise_gpu_ctx_create(0, None) == noise_amd.E_ARG
+    assert lib.noise_gpu_ctx_destroy(None) == noise_amd.OK
+    buf = ctypes.create_string_buffer(64)
+    assert lib.noise_gpu_ctx_encrypt_host(None, bytes(range(32)), 0, None, 0, buf, 16) == noise_amd.E_ARG
+    assert lib.noise_gpu_ctx_rekey_host(None, buf) == noise_amd.E_ARG
+
+
 def test_cipherstate_host_rules():
     """noise::CipherState rules that run before any device call: spec
     has_key, the 2^64-2 nonce limit (noise.cpp:398), 40-byte layout."""

@@ -374,6 +374,57 @@ def test_host_pipeline_matches_device(oracle):
             key, 10 + i, b"", pt[i * L:(i + 1) * L].numpy().tobytes())
 
 
+def test_device_context_api(oracle, golden):
+    """noise_gpu_ctx_*: an explicit device context gives the context-free
+    entry points' results (single records, rekey, descriptor and uniform host
+    batches), keeps the caller's current device, and refuses bad indices."""
+    import ctypes
+    lib = noise_amd.load()
+    h = ctypes.c_void_p()
+    assert lib.noise_gpu_ctx_create(torch.cuda.device_count(), ctypes.byref(h)) == noise_amd.E_ARG
+    assert lib.noise_gpu_ctx_create(0, ctypes.byref(h)) == 0 and h.value
+    try:
+        d = ctypes.c_int(-1)
+        assert lib.noise_gpu_ctx_device(h, ctypes.byref(d)) == 0 and d.value == 0
+        rng = random.Random(21)
+        key = rng.randbytes(32)
+        for L, A in ((0, 0), (33, 64), (1024, 0), (20000, 9000), (70000, 0)):
+            pt, ad = rng.randbytes(L), rng.randbytes(A)
+            buf = ctypes.create_string_buffer(pt, L + 16)
+            assert lib.noise_gpu_ctx_encrypt_host(h, key, 5, ad or None, A, buf, L) == 0
+            assert buf.raw == oracle.encrypt(key, 5, ad, pt)
+            assert lib.noise_gpu_ctx_decrypt_host(h, key, 5, ad or None, A, buf, L + 16) == 0
+            assert buf.raw[:L] == pt
+        kb = ctypes.create_string_buffer(bytes(32), 32)
+        assert lib.noise_gpu_ctx_rekey_host(h, kb) == 0
+        assert kb.raw.hex() == oracle_lib.KAT_K4_REKEY_ZERO
+        recs = golden["transport"][:300]
+        keys, dsc, inb, adb, out_bytes = pack_records(recs)
+        out = ctypes.create_string_buffer(out_bytes)
+        dbuf = dsc.view(np.uint8).tobytes()
+        assert lib.noise_gpu_ctx_encrypt_records_host(h, keys, len(recs), dbuf, len(recs), inb,
+                                                      len(inb), out, out_bytes, adb or None,
+                                                      len(adb)) == 0
+        for i, r in enumerate(recs):
+            o = int(dsc[i]["out_off"])
+            assert out.raw[o:o + len(r["pt"]) + 16] == r["ct"]
+        R, L = 500, 1024
+        pt = rng.randbytes(R * L)
+        ct = ctypes.create_string_buffer(R * (L + 16))
+        back = ctypes.create_string_buffer(R * L)
+        st = ctypes.create_string_buffer(b"\x09" * R, R)
+        secs = ctypes.c_double()
+        assert lib.noise_gpu_ctx_encrypt_uniform_host(h, key, 9, pt, L, ct, L + 16, L, R,
+                                                      ctypes.byref(secs)) == 0
+        assert lib.noise_gpu_ctx_decrypt_uniform_host(h, key, 9, ct, L + 16, back, L, L, st, R,
+                                                      ctypes.byref(secs)) == 0
+        assert back.raw == pt and st.raw == bytes(R)
+        assert ct.raw[(R - 1) * (L + 16):] == oracle.encrypt(key, 9 + R - 1, b"", pt[(R - 1) * L:])
+        assert torch.cuda.current_device() == 0
+    finally:
+        assert lib.noise_gpu_ctx_destroy(h) == 0
+
+
 def test_cipherstate_cpp_surface():
     """The drop-in noise::CipherState (C++20) on the golden records."""
     exe = os.path.join(noise_amd.ROOT, "noise-cpp_amd", "bin", "cipherstate_test")

@@ -158,6 +158,53 @@ int main() {
     for (uint32_t i = 0; i < R; ++i) CHECK(st[i] == 0, "uniform_host status %u", i);
     scan("decrypt_uniform_host");
   }
+  // ---- explicit device context: same results through its own staging
+  {
+    noise_gpu_ctx *ctx = nullptr;
+    CHECK(noise_gpu_ctx_create(0, &ctx) == NOISE_GPU_OK && ctx, "ctx_create");
+    CHECK(noise_gpu_ctx_create(5, &ctx) == NOISE_GPU_E_ARG, "ctx_create bad index");
+    CHECK(noise_gpu_ctx_create(0, &ctx) == NOISE_GPU_OK && ctx, "ctx_create again");
+    int dev = -1;
+    CHECK(noise_gpu_ctx_device(ctx, &dev) == NOISE_GPU_OK && dev == 0, "ctx_device");
+    for (size_t L : {0, 17, 1024, 70000}) {
+      const auto pt = rbytes(L), ad = rbytes(64);
+      std::vector<uint8_t> want(L + 16), buf(pt);
+      buf.resize(L + 16);
+      oracle_noise_encrypt(key, 99, ad.data(), 64, pt.data(), L, want.data());
+      ++calls;
+      int rc = noise_gpu_ctx_encrypt_host(ctx, key, 99, ad.data(), 64, buf.data(), L);
+      CHECK(rc == NOISE_GPU_OK && buf == want, "ctx encrypt_host L=%zu rc=%d", L, rc);
+      scan("ctx encrypt_host");
+      ++calls;
+      rc = noise_gpu_ctx_decrypt_host(ctx, key, 99, ad.data(), 64, buf.data(), L + 16);
+      CHECK(rc == NOISE_GPU_OK && std::memcmp(buf.data(), pt.data(), L) == 0,
+            "ctx decrypt_host L=%zu rc=%d", L, rc);
+      scan("ctx decrypt_host");
+    }
+    {
+      const uint32_t L = 1024, R = 100;
+      const auto pt = rbytes((size_t)L * R);
+      std::vector<uint8_t> ct((size_t)(L + 16) * R), back((size_t)L * R), st(R, 9);
+      double secs = 0;
+      ++calls;
+      int rc = noise_gpu_ctx_encrypt_uniform_host(ctx, key, 3, pt.data(), L, ct.data(), L + 16, L,
+                                                  R, &secs);
+      std::vector<uint8_t> w(L + 16);
+      oracle_noise_encrypt(key, 3 + R - 1, nullptr, 0, pt.data() + (size_t)(R - 1) * L, L, w.data());
+      CHECK(rc == NOISE_GPU_OK &&
+                std::memcmp(ct.data() + (size_t)(R - 1) * (L + 16), w.data(), L + 16) == 0,
+            "ctx encrypt_uniform_host rc=%d", rc);
+      scan("ctx encrypt_uniform_host");
+      ++calls;
+      rc = noise_gpu_ctx_decrypt_uniform_host(ctx, key, 3, ct.data(), L + 16, back.data(), L, L,
+                                              st.data(), R, &secs);
+      CHECK(rc == NOISE_GPU_OK && back == pt, "ctx decrypt_uniform_host rc=%d", rc);
+      scan("ctx decrypt_uniform_host");
+    }
+    CHECK(noise_gpu_ctx_destroy(ctx) == NOISE_GPU_OK, "ctx_destroy");
+    CHECK(noise_gpu_ctx_encrypt_host(nullptr, key, 0, nullptr, 0, nullptr, 0) == NOISE_GPU_E_ARG,
+          "null ctx");
+  }
   if (fails) {
     std::printf("emu_api FAIL (%d failures, %d calls, %d scans)\n", fails, calls, scans);
     return 1;

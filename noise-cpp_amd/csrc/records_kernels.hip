@@ -462,8 +462,8 @@ __global__ __launch_bounds__(64) void k_seg_tail(const uint32_t *__restrict__ ta
 template <bool DECRYPT>
 __global__ __launch_bounds__(64) void k_seg_finalize(
     const uint32_t *__restrict__ fin, const SegRec *__restrict__ rt,
-    const SegPartial *__restrict__ partial, const RecHdr *hdr, const uint8_t *in, uint8_t *out,
-    uint8_t *status) {
+    const SegPartial *__restrict__ partial, const uint32_t *__restrict__ partial_hi,
+    const RecHdr *hdr, const uint8_t *in, uint8_t *out, uint8_t *status) {
   const uint64_t n = hdr->counts[kClsLong], nlong = hdr->nlong;
 #pragma unroll 1
   for (uint64_t t = (uint64_t)blockIdx.x * 64 + threadIdx.x; t < n;
@@ -477,7 +477,7 @@ __global__ __launch_bounds__(64) void k_seg_finalize(
     const uint32_t nf = R.nfull;
     {
       const SegPartial &P0 = partial[R.seg0];
-      acc = to26(P0.h[0], P0.h[1], P0.h[2], P0.h[3], P0.h[4]);
+      acc = to26(P0.h[0], P0.h[1], P0.h[2], P0.h[3], partial_hi[R.seg0]);
     }
     // Horner in R over the partial sums, 8 segments per step: the 8 loads
     // are issued together (the loop is load-latency bound otherwise: one
@@ -491,7 +491,7 @@ __global__ __launch_bounds__(64) void k_seg_finalize(
       for (int j = 0; j < 8; ++j) {
         const SegPartial &P = partial[R.seg0 + s + j];
         lo[j] = make_uint4(P.h[0], P.h[1], P.h[2], P.h[3]);
-        hi[j] = P.h[4];
+        hi[j] = partial_hi[R.seg0 + s + j];
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -506,7 +506,7 @@ __global__ __launch_bounds__(64) void k_seg_finalize(
     for (; s < nf; ++s) {
       const SegPartial &P = partial[R.seg0 + s];
       acc = mul26(acc, R64);
-      const F26 t = to26(P.h[0], P.h[1], P.h[2], P.h[3], P.h[4]);
+      const F26 t = to26(P.h[0], P.h[1], P.h[2], P.h[3], partial_hi[R.seg0 + s]);
 #pragma unroll
       for (int i = 0; i < 5; ++i) acc.a[i] += t.a[i];
       carry26(acc);
@@ -566,8 +566,8 @@ __global__ __launch_bounds__(64) void k_seg_finalize(
 template <bool DECRYPT, int W>
 __global__ __launch_bounds__(64) void k_seg_finalize_w(
     const uint32_t *__restrict__ fin, const SegRec *__restrict__ rt,
-    const SegPartial *__restrict__ partial, RecHdr *hdr, const uint8_t *in, uint8_t *out,
-    uint8_t *status) {
+    const SegPartial *__restrict__ partial, const uint32_t *__restrict__ partial_hi,
+    RecHdr *hdr, const uint8_t *in, uint8_t *out, uint8_t *status) {
   static_assert(W == 2 || W == 4 || W == 8, "lanes per record");
   constexpr int LOGW = W == 2 ? 1 : (W == 4 ? 2 : 3);
   constexpr uint32_t KMAX = (63u + W - 1u) / W;  // segments per lane (nf <= 63)
@@ -605,7 +605,7 @@ __global__ __launch_bounds__(64) void k_seg_finalize_w(
       if (k < K) {
         const SegPartial &P = partial[seg0 + i + W * k];
         lo[k] = make_uint4(P.h[0], P.h[1], P.h[2], P.h[3]);
-        hi[k] = P.h[4];
+        hi[k] = partial_hi[seg0 + i + W * k];
       }
     }
 #pragma unroll
@@ -946,15 +946,15 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   hipLaunchKernelGGL((k_aead_tile<DECRYPT, 1024, false, kTileSeg>), gseg, bt, 0, stream, a);
   if ((e = hipStreamWaitEvent(stream, ax.join, 0)) != hipSuccess) return e;
 #ifdef NOISE_FIN_LANE  // A/B: one lane per long record
-  hipLaunchKernelGGL((k_seg_finalize<DECRYPT>), grid, bt, 0, stream, fin, ta.rt, ta.partial, hdr,
-                     in, out, status);
+  hipLaunchKernelGGL((k_seg_finalize<DECRYPT>), grid, bt, 0, stream, fin, ta.rt, ta.partial,
+                     ta.partial_hi, hdr, in, out, status);
 #else
 #ifndef NOISE_FIN_W
 #define NOISE_FIN_W 4
 #endif
   const dim3 gfin(capped((nrec + 64 / NOISE_FIN_W - 1) / (64 / NOISE_FIN_W), NOISE_GRID_CAP));
   hipLaunchKernelGGL((k_seg_finalize_w<DECRYPT, NOISE_FIN_W>), gfin, bt, 0, stream, fin, ta.rt,
-                     ta.partial, const_cast<RecHdr *>(hdr), in, out, status);
+                     ta.partial, ta.partial_hi, const_cast<RecHdr *>(hdr), in, out, status);
 #endif
   if (DECRYPT) {
     const dim3 gfix(capped((segbound + nrec + 63) / 64, NOISE_GRID_CAP));
@@ -988,7 +988,8 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   const uint64_t segcap = nrec * 63 < kSegCapMax ? nrec * 63 : kSegCapMax;
 
   // scratch: header | part[nw][kCols] | wbase[nw][kCols] | idx[nrec] |
-  //          tails[nrec] | fin[nrec] | rt[nrec] | segs[segcap] | partial[segcap]
+  //          tails[nrec] | fin[nrec] | rt[nrec] | segs[segcap] | partial[segcap] |
+  //          partial_hi[segcap]
   const uint64_t o_part = sizeof(RecHdr);
   const uint64_t o_wbase = align_up(o_part + nw * kCols * 4, 256);
   const uint64_t o_idx = align_up(o_wbase + nw * kCols * 8, 256);
@@ -997,7 +998,8 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   const uint64_t o_rt = align_up(o_fin + nrec * 4, 256);
   const uint64_t o_segs = align_up(o_rt + nrec * sizeof(SegRec), 256);
   const uint64_t o_part2 = align_up(o_segs + segcap * sizeof(SegEntry), 256);
-  const uint64_t bytes = o_part2 + segcap * sizeof(SegPartial);
+  const uint64_t o_phi = align_up(o_part2 + segcap * sizeof(SegPartial), 256);
+  const uint64_t bytes = o_phi + segcap * sizeof(uint32_t);
   void *mem = nullptr;
   hipError_t e = scratch_get(&mem, bytes, stream);
   if (e != hipSuccess) return e;
@@ -1011,6 +1013,7 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   SegRec *rt = reinterpret_cast<SegRec *>(base + o_rt);
   SegEntry *segs = reinterpret_cast<SegEntry *>(base + o_segs);
   SegPartial *partial = reinterpret_cast<SegPartial *>(base + o_part2);
+  uint32_t *partial_hi = reinterpret_cast<uint32_t *>(base + o_phi);
 
   const dim3 b64(64);
   hipLaunchKernelGGL(k_cls_count, dim3((unsigned)nw), b64, 0, stream, recs, nrec, (uint32_t)chunk, keys, nkeys, in, out, part);
@@ -1030,6 +1033,7 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   ta.segs = segs;
   ta.rt = rt;
   ta.partial = partial;
+  ta.partial_hi = partial_hi;
   ta.nseg = &hdr->nseg;
   return decrypt ? launch_classes<true>(ta, nrec, hdr, keys, nkeys, recs, idx, tails, fin, segcap,
                                        in, out, ad, status, stream)

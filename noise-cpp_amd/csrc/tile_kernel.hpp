@@ -105,8 +105,8 @@ static_assert(sizeof(SegRec) == 224, "SegRec layout");
 struct SegEntry {                // one per full segment
   uint32_t q, s;                 // long-record index, segment number
 };
-struct SegPartial {              // P_s in radix 2^32 (h4 small)
-  uint32_t h[8];
+struct SegPartial {              // P_s in radix 2^32: words h0..h3 (h4, small,
+  uint32_t h[4];                 // in a separate array: 20 B per segment)
 };
 
 struct TileArgs {
@@ -130,7 +130,8 @@ struct TileArgs {
   int cls;                       // kTileDesc: this launch's class
   const SegEntry *segs;          // kTileSeg
   const SegRec *rt;              // kTileSeg
-  SegPartial *partial;           // kTileSeg
+  SegPartial *partial;           // kTileSeg: P_s words 0..3
+  uint32_t *partial_hi;          // kTileSeg: P_s word 4
   const unsigned long long *nseg;  // kTileSeg: number of segments (device)
 };
 
@@ -547,10 +548,10 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
       // the segment's partial sum (no length block, no s); lane 0 of the
       // segment stores it
       if (j == 0 && valid) {
-        const u32x4 w0 = {p.h0, p.h1, p.h2, p.h3}, w1 = {p.h4, 0u, 0u, 0u};
-        g_u32x4 *dp = (g_u32x4 *)(a.partial + (super0 + (uint64_t)t * C::RPT + rho));
-        __builtin_nontemporal_store(w0, dp);
-        __builtin_nontemporal_store(w1, dp + 1);
+        const u32x4 w0 = {p.h0, p.h1, p.h2, p.h3};
+        const uint64_t g = super0 + (uint64_t)t * C::RPT + rho;
+        __builtin_nontemporal_store(w0, (g_u32x4 *)(a.partial + g));
+        __builtin_nontemporal_store(p.h4, (__attribute__((address_space(1))) uint32_t *)(a.partial_hi + g));
       }
     } else {
       poly_block(p, 0u, 0u, (uint32_t)L, 0u);  // LE64(ad_len = 0) || LE64(L)

@@ -301,7 +301,12 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
   // within one 64-slot group: bank-conflict free; destination uniform), the
   // last one the tile's RPT tags.  Otherwise instruction q stores pieces
   // 64q..64q+63 of the tile's output in wire order (ct || tag interleaved).
-  constexpr bool RECW = CONTIG && !DECRYPT && C::SPR >= 64 && C::SPR % 64 == 0;
+  // Strided layouts (in-place batches, padded strides) take it too: their
+  // wire-order gather (a division by SPR + 1 and a 64-bit address per lane
+  // and instruction) pushed the keyed encrypt kernels past 256 VGPRs, i.e.
+  // to one wave per SIMD.  Not kTileDesc / kTileSeg (RECQ below).
+  constexpr bool RECW = !DECRYPT && !SEG && MODE != kTileDesc && C::SPR >= 64 &&
+                        C::SPR % 64 == 0;
   constexpr int NDATA = C::RPT * C::SPR / 64;
   constexpr int NOUT = RECW ? NDATA + 1 : (OUT_SLOTS + 63) / 64;  // store instructions
   static_assert(!(CONTIG && (MODE == kTileDesc || SEG)), "descriptor tiles are strided");

@@ -58,7 +58,9 @@ class Batcher {
   };
 
   explicit Batcher(Direction d) : dir_(d) {}
-  // register a session: its key and next nonce (copied); returns its id
+  // register a session: its key and next nonce (copied); returns its id.
+  // Throws invalid_argument for a CipherState without a key (has_key()
+  // false): the GPU never uses an all-zero key row.
   std::size_t add_session(const CipherState &cs);
   // queue one message of session s (plaintext / ct || tag)
   void submit(std::size_t s, std::vector<std::uint8_t> msg);
@@ -133,6 +135,7 @@ class Pipeline {
   Pipeline(const Pipeline &) = delete;
   Pipeline &operator=(const Pipeline &) = delete;
 
+  // as Batcher::add_session (a keyless CipherState throws invalid_argument)
   std::size_t add_session(const CipherState &cs);
   // copy one message into the filling slot and assign its nonce; false (and
   // nothing consumed) when the slot has no room -- flush() and retry

@@ -44,7 +44,18 @@ bool Deframer::next(std::vector<std::uint8_t> &msg) {
   return true;
 }
 
+// A session without a key (HasKey() false: an all-zero key) is refused.  The
+// batch kernels never use an all-zero key row (they write nothing and report
+// NOISE_GPU_REC_BAD_KEY), so such a session's results would be garbage
+// reported as valid ciphertext; the reference CipherState would instead pass
+// the plaintext through unencrypted (noise.cpp:395-397), which a batch API
+// must not do silently either.
+static void require_key(const CipherState &cs) {
+  if (!cs.has_key()) throw std::invalid_argument("transport: session has no key");
+}
+
 std::size_t Batcher::add_session(const CipherState &cs) {
+  require_key(cs);
   sessions_.push_back({cs.key_material(), cs.nonce()});
   return sessions_.size() - 1;
 }
@@ -302,6 +313,7 @@ void Pipeline::grow_keys() {
 }
 
 std::size_t Pipeline::add_session(const CipherState &cs) {
+  require_key(cs);
   const std::size_t s = nonces_.size();
   if (s >= 0xffffffffu) throw std::length_error("pipeline: too many sessions");
   if (s == key_cap_) grow_keys();

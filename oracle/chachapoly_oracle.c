@@ -17,6 +17,8 @@
  *   poly1305_*             crypto_poly1305_init/update/final, lock_auth
  *                                                    monocypher.c:366-440, 2858-2873
  *   oracle_rekey           CipherState::rekey        noise.cpp:429-439
+ *   oracle_check_records / oracle_check_uniform: the above per record over
+ *                          a whole GPU batch (full-size parity tests)
  *
  * The arithmetic is written independently (RFC 8439 structure; Poly1305 in
  * 3 x 44-bit limbs with 128-bit products, unlike monocypher's 5 x 32-bit
@@ -30,6 +32,7 @@
 #include <pthread.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 #include <time.h>
 
@@ -294,4 +297,159 @@ double oracle_batch_uniform(int decrypt, const uint8_t key[32], uint64_t n0,
   for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
   clock_gettime(CLOCK_MONOTONIC, &t1);
   return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
+/* ---- whole-batch parity checkers (tests/: full-size configs) ------------
+ * Every record of a batch the GPU processed is recomputed here and compared
+ * byte for byte.  Descriptors use the C-ABI layout of noise_gpu_record
+ * (include/noise_gpu.h: in_off, out_off, nonce, ad_off u64; len, ad_len,
+ * key_idx, reserved u32 = 48 B), restated so this file needs no product
+ * header.  `in` / `out` may be windows of larger buffers: a descriptor's
+ * offset minus in_base / out_base indexes them (chunked device-to-host
+ * copies).  Encrypt (decrypt = 0): out[out_off .. +len+16) must equal
+ * ENCRYPT(key, nonce, ad, in[in_off .. +len)).  Decrypt (decrypt = 1):
+ * status[i] must be 0 and out[out_off .. +len) the plaintext where the tag
+ * verifies, 1 (NOISE_GPU_REC_BAD_MAC) where it does not, 2 for a key index
+ * past the table or an all-zero key row (NOISE_GPU_REC_BAD_KEY).  Returns
+ * the number of mismatching records; *first_bad receives the lowest index
+ * of one (or -1). */
+typedef struct {
+  uint64_t in_off, out_off, nonce, ad_off;
+  uint32_t len, ad_len, key_idx, reserved;
+} oracle_rec_t;
+
+typedef struct {
+  int decrypt;
+  const uint8_t *keys;
+  uint32_t nkeys;
+  const oracle_rec_t *recs;
+  uint64_t in_base, out_base;
+  const uint8_t *in, *ad;
+  const uint8_t *out, *status;
+  /* uniform form (recs == NULL): one key, nonce n0 + i, strided records */
+  const uint8_t *key;
+  uint64_t n0, in_stride, out_stride;
+  uint32_t len;
+  uint64_t lo, hi;
+  int64_t bad, first;
+} check_t;
+
+static int zero_key(const uint8_t *k) {
+  uint8_t acc = 0;
+  for (int i = 0; i < 32; ++i) acc |= k[i];
+  return acc == 0;
+}
+
+static void *run_check(void *arg) {
+  check_t *c = (check_t *)arg;
+  uint8_t *buf = NULL;
+  size_t cap = 0;
+  for (uint64_t i = c->lo; i < c->hi; ++i) {
+    oracle_rec_t d;
+    const uint8_t *key;
+    if (c->recs) {
+      d = c->recs[i];
+      key = d.key_idx < c->nkeys ? c->keys + 32ull * d.key_idx : NULL;
+    } else {
+      d.in_off = i * c->in_stride;
+      d.out_off = i * c->out_stride;
+      d.nonce = c->n0 + i;
+      d.ad_off = 0;
+      d.len = c->len;
+      d.ad_len = 0;
+      key = c->key;
+    }
+    const uint8_t *in = c->in + (d.in_off - c->in_base);
+    const uint8_t *out = c->out + (d.out_off - c->out_base);
+    const uint8_t *ad = d.ad_len ? c->ad + d.ad_off : NULL;
+    size_t need = (size_t)d.len + 16;
+    if (need > cap) {
+      free(buf);
+      cap = need < 65552 ? 65552 : need;
+      buf = (uint8_t *)malloc(cap);
+    }
+    int ok;
+    if (!key || zero_key(key)) {
+      /* encrypt: the GPU writes nothing for such a record (not checked
+       * here); decrypt: status BAD_KEY */
+      ok = !c->decrypt || c->status[i] == 2;
+    } else if (!c->decrypt) {
+      oracle_noise_encrypt(key, d.nonce, ad, d.ad_len, in, d.len, buf);
+      ok = memcmp(buf, out, need) == 0;
+    } else {
+      int rc = oracle_noise_decrypt(key, d.nonce, ad, d.ad_len, in, need, buf);
+      ok = rc == 0 ? (c->status[i] == 0 && memcmp(buf, out, d.len) == 0)
+                   : c->status[i] == 1;
+    }
+    if (!ok) {
+      if (c->first < 0) c->first = (int64_t)i;
+      c->bad++;
+    }
+  }
+  free(buf);
+  return NULL;
+}
+
+static int64_t check_threads(check_t proto, uint64_t nrec, int threads, int64_t *first_bad) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  if ((uint64_t)threads > nrec) threads = nrec ? (int)nrec : 1;
+  pthread_t tid[256];
+  check_t jobs[256];
+  for (int t = 0; t < threads; ++t) {
+    jobs[t] = proto;
+    jobs[t].lo = nrec * t / threads;
+    jobs[t].hi = nrec * (t + 1) / threads;
+    jobs[t].bad = 0;
+    jobs[t].first = -1;
+    pthread_create(&tid[t], NULL, run_check, &jobs[t]);
+  }
+  int64_t bad = 0, first = -1;
+  for (int t = 0; t < threads; ++t) {
+    pthread_join(tid[t], NULL);
+    bad += jobs[t].bad;
+    if (jobs[t].first >= 0 && (first < 0 || jobs[t].first < first)) first = jobs[t].first;
+  }
+  if (first_bad) *first_bad = first;
+  return bad;
+}
+
+int64_t oracle_check_records(int decrypt, const uint8_t *keys, uint32_t nkeys,
+                             const void *recs, uint64_t nrec, uint64_t in_base,
+                             const uint8_t *in, uint64_t out_base, const uint8_t *out,
+                             const uint8_t *ad, const uint8_t *status, int threads,
+                             int64_t *first_bad) {
+  check_t c;
+  memset(&c, 0, sizeof c);
+  c.decrypt = decrypt;
+  c.keys = keys;
+  c.nkeys = nkeys;
+  c.recs = (const oracle_rec_t *)recs;
+  c.in_base = in_base;
+  c.out_base = out_base;
+  c.in = in;
+  c.out = out;
+  c.ad = ad;
+  c.status = status;
+  return check_threads(c, nrec, threads, first_bad);
+}
+
+/* uniform form: record i at in + i * in_stride / out + i * out_stride, nonce
+ * n0 + i, one key, no AD (status indexed from 0 like the records) */
+int64_t oracle_check_uniform(int decrypt, const uint8_t key[32], uint64_t n0,
+                             const uint8_t *in, uint64_t in_stride, const uint8_t *out,
+                             uint64_t out_stride, uint32_t len, uint64_t nrec,
+                             const uint8_t *status, int threads, int64_t *first_bad) {
+  check_t c;
+  memset(&c, 0, sizeof c);
+  c.decrypt = decrypt;
+  c.key = key;
+  c.n0 = n0;
+  c.in = in;
+  c.out = out;
+  c.in_stride = in_stride;
+  c.out_stride = out_stride;
+  c.len = len;
+  c.status = status;
+  return check_threads(c, nrec, threads, first_bad);
 }

@@ -505,6 +505,29 @@ int main(int argc, char **argv) {
     threw = true;
   }
   check(threw, "frame > 65535 refused", 0);
+  // a session without a key (all-zero k, HasKey() false) is refused by both
+  // batch objects instead of producing unkeyed "ciphertext" 
+  {
+    noise::CipherState nokey;
+    for (int which = 0; which < 2; ++which) {
+      threw = false;
+      try {
+        if (which == 0) {
+          nt::Batcher b(nt::Batcher::Direction::Encrypt);
+          b.add_session(nokey);
+        } else {
+          nt::Pipeline::Options po;
+          po.depth = 2;
+          po.slot_records = 16;
+          nt::Pipeline p(nt::Pipeline::Direction::Encrypt, po);
+          p.add_session(nokey);
+        }
+      } catch (const std::invalid_argument &) {
+        threw = true;
+      }
+      check(threw, which ? "pipeline refuses a keyless session" : "batcher refuses a keyless session", which);
+    }
+  }
   std::printf("sessions %d messages %d: %s (%d failures)\n", S, M, fails ? "FAIL" : "ok", fails);
   return fails ? 1 : 0;
 }

@@ -35,6 +35,16 @@ def k5_plaintext():
     return bytes((7 * j + 3) % 256 for j in range(1024))
 
 
+def check_threads():
+    """Checker threads: the CPUs this process may run on, at most 16 (a GPU
+    box's CPU share; os.cpu_count() there reports the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
 def _build():
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "all"], check=True)
 
@@ -58,6 +68,18 @@ class Oracle:
                                            ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64,
                                            ctypes.c_int, ctypes.c_void_p]
         L.oracle_batch_uniform.restype = ctypes.c_double
+        L.oracle_check_records.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32,
+                                           ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                           ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                           ctypes.POINTER(ctypes.c_int64)]
+        L.oracle_check_records.restype = ctypes.c_int64
+        L.oracle_check_uniform.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_uint64,
+                                           ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                           ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                           ctypes.c_void_p, ctypes.c_int,
+                                           ctypes.POINTER(ctypes.c_int64)]
+        L.oracle_check_uniform.restype = ctypes.c_int64
         self.ref = None
         if os.path.exists(REF_SO):
             R = ctypes.CDLL(REF_SO)
@@ -108,6 +130,36 @@ class Oracle:
         out = ctypes.create_string_buffer(max(nbytes, 1))
         self.lib.oracle_fill_synthetic(out, offset, nbytes, seed)
         return out.raw[:nbytes]
+
+    def check_records(self, decrypt, keys, nkeys, recs, inb, outb, ad=None, status=None,
+                      in_base=0, out_base=0, threads=None):
+        """Whole-batch parity: every descriptor of `recs` (numpy noise_gpu_record
+        array) recomputed and compared.  keys/inb/outb/ad/status are numpy uint8
+        arrays (C-contiguous).  Returns (mismatching records, first mismatching
+        index or -1)."""
+        first = ctypes.c_int64(-1)
+
+        def ptr(a):
+            if a is None:
+                return None
+            assert a.flags["C_CONTIGUOUS"]
+            return a.ctypes.data
+        bad = self.lib.oracle_check_records(int(decrypt), ptr(keys), nkeys, ptr(recs), len(recs),
+                                            in_base, ptr(inb), out_base, ptr(outb), ptr(ad),
+                                            ptr(status), threads or check_threads(),
+                                            ctypes.byref(first))
+        return int(bad), first.value
+
+    def check_uniform(self, decrypt, key, n0, inb, in_stride, outb, out_stride, length, nrec,
+                      status=None, threads=None):
+        """Whole-batch parity of a uniform batch (record i: nonce n0 + i)."""
+        first = ctypes.c_int64(-1)
+        bad = self.lib.oracle_check_uniform(int(decrypt), bytes(key), n0 % (1 << 64),
+                                            inb.ctypes.data, in_stride, outb.ctypes.data,
+                                            out_stride, length, nrec,
+                                            None if status is None else status.ctypes.data,
+                                            threads or check_threads(), ctypes.byref(first))
+        return int(bad), first.value
 
     def encrypt_uniform_np(self, key, n0, pt, length, in_stride, out_stride, nrec, threads=8):
         """Uniform batch on numpy buffers (parity tests at moderate sizes)."""

@@ -327,8 +327,10 @@ def test_fill_synthetic_matches_oracle(oracle):
 
 def test_config2_full_size_round_trip(oracle):
     """BASELINE config 2 at full size: 2^20 x 1 KiB, one key, nonces 0..R-1.
-    Size-independent properties: every tag verifies, decrypt(encrypt(x)) == x,
-    and a random sample (plus the first/last records) equals the oracle."""
+    Every record of both directions bit-exact against the oracle (chunked
+    D2H + oracle_check_uniform), plus the size-independent properties: every
+    tag verifies, decrypt(encrypt(x)) == x."""
+    import fullcheck
     R, L = 1 << 20, 1024
     key = bytes(range(32))
     d_pt = torch.empty(R * L, dtype=torch.uint8, device="cuda")
@@ -341,11 +343,12 @@ def test_config2_full_size_round_trip(oracle):
     torch.cuda.synchronize()
     assert int(d_st.sum().item()) == 0
     assert torch.equal(d_pt, d_back)
-    ct = d_ct.view(R, L + 16)
-    rng = random.Random(2)
-    for i in rng.sample(range(R), 256) + [0, R - 1]:
-        p = oracle.synthetic(L, SEED, offset=i * L)
-        assert ct[i].cpu().numpy().tobytes() == oracle.encrypt(key, i, b"", p), i
+    fullcheck.check_uniform(oracle, torch, key, 0, d_pt, L, d_ct, L + 16, L, R)
+    fullcheck.check_uniform(oracle, torch, key, 0, d_ct, L + 16, d_back, L, L, R, decrypt=True,
+                            d_status=d_st)
+    # the device generator is the one the oracle restates
+    for i in (0, 12345, R - 1):
+        assert d_pt[i * L:(i + 1) * L].cpu().numpy().tobytes() == oracle.synthetic(L, SEED, i * L)
 
 
 def test_host_pipeline_matches_device(oracle):

@@ -136,8 +136,9 @@ int main() {
     scan(big ? "encrypt_records_host (classified)" : "encrypt_records_host (small)");
   }
   // ---- uniform batch between host buffers (pipeline; the tile kernel's
-  // wire-order gather below 1 KiB, the record-wise one from 1 KiB)
-  for (uint32_t L : {256u, 1024u, 4096u}) {
+  // wire-order gather below 1 KiB, the record-wise one from 1 KiB), at
+  // every length the tile kernel serves: G = 1 .. 64 lanes per record
+  for (uint32_t L : {64u, 128u, 192u, 256u, 512u, 1024u, 2048u, 4096u, 8192u, 16384u}) {
     const uint32_t R = L >= 4096 ? 70 : 300;
     const auto pt = rbytes((size_t)L * R);
     std::vector<uint8_t> ct((size_t)(L + 16) * R), back((size_t)L * R), st(R, 9);
@@ -146,7 +147,7 @@ int main() {
     int rc = noise_gpu_encrypt_uniform_host(key, 7, pt.data(), L, ct.data(), L + 16, L, R, &secs);
     CHECK(rc == NOISE_GPU_OK, "encrypt_uniform_host rc=%d", rc);
     std::vector<uint8_t> w(L + 16);
-    for (uint32_t i = 0; i < R; i += 37) {
+    for (uint32_t i = 0; i < R; ++i) {
       oracle_noise_encrypt(key, 7 + i, nullptr, 0, pt.data() + (size_t)i * L, L, w.data());
       CHECK(std::memcmp(ct.data() + (size_t)i * (L + 16), w.data(), L + 16) == 0, "uniform_host %u", i);
     }
@@ -162,6 +163,7 @@ int main() {
   {
     noise_gpu_ctx *ctx = nullptr;
     CHECK(noise_gpu_ctx_create(0, &ctx) == NOISE_GPU_OK && ctx, "ctx_create");
+    CHECK(noise_gpu_ctx_destroy(ctx) == NOISE_GPU_OK, "ctx_destroy");
     CHECK(noise_gpu_ctx_create(5, &ctx) == NOISE_GPU_E_ARG, "ctx_create bad index");
     CHECK(noise_gpu_ctx_create(0, &ctx) == NOISE_GPU_OK && ctx, "ctx_create again");
     int dev = -1;

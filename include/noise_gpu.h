@@ -92,7 +92,13 @@ int noise_gpu_device_count(int *count);
  * 16-byte aligned pointers/strides, ad_len == 0 and len in {64, 128, 192,
  * 256, 512, 1024, 2048, 4096, 8192, 16384} run on the LDS-staged tile kernel
  * (the hot path); other shapes one record per lane (vector path when 16-byte
- * aligned with len % 16 == 0, byte-granular otherwise). */
+ * aligned with len % 16 == 0, byte-granular otherwise).
+ * Key handling: h_key is copied into the kernel's argument block (kernarg
+ * memory) by value, so the 32-byte key stays in that launch's kernarg
+ * segment after the call, like any kernel argument; the runtime reuses,
+ * but does not wipe, kernarg memory.  Callers that must not leave a key
+ * there use the sessions / descriptor functions, whose keys live in a
+ * device key table the caller owns and wipes. */
 int noise_gpu_encrypt_uniform(const uint8_t h_key[32], uint64_t nonce0,
                               const uint8_t *d_in, uint64_t in_stride,
                               uint8_t *d_out, uint64_t out_stride,
@@ -325,7 +331,17 @@ int noise_gpu_decrypt_records_host(const uint8_t *h_keys, uint32_t nkeys,
  * current device) that persists across calls (created on the thread's first
  * call on that device; a thread serving several GPUs keeps one per device);
  * their contents are zeroed at the end of every call.  The single-record
- * and descriptor host entry points above keep their staging the same way. */
+ * and descriptor host entry points above keep their staging the same way.
+ * Footprint of that per-(thread, device) state: the uniform pipeline holds
+ * 3 x 34 MiB of device memory and 3 streams; the descriptor path a device
+ * staging buffer sized by the largest call plus its records scratch (about
+ * 2 KiB per record of that call) and a companion stream; the single-record
+ * path a pinned buffer.  It lives until the thread exits or calls
+ * noise_gpu_thread_release() -- thread-pool servers should call that, or
+ * use an explicit noise_gpu_ctx (below), whose destroy frees the same.
+ * len is at most NOISE_GPU_UNIFORM_HOST_MAX_LEN (NOISE_GPU_E_ARG above it;
+ * a Noise record is at most 65519 bytes). */
+#define NOISE_GPU_UNIFORM_HOST_MAX_LEN (8u << 20)
 int noise_gpu_encrypt_uniform_host(const uint8_t h_key[32], uint64_t nonce0,
                                    const uint8_t *h_in, uint64_t in_stride,
                                    uint8_t *h_out, uint64_t out_stride,
@@ -336,6 +352,13 @@ int noise_gpu_decrypt_uniform_host(const uint8_t h_key[32], uint64_t nonce0,
                                    uint8_t *h_out, uint64_t out_stride,
                                    uint32_t len, uint8_t *h_status,
                                    uint64_t nrec, double *seconds);
+
+/* Wipe and free every per-(calling thread, device) context the host-buffer
+ * entry points created for this thread (staging, records scratch and its
+ * companion stream, the latency-path buffer, the uniform pipeline), on all
+ * devices.  The next call re-creates what it needs.  Synchronises the
+ * thread's streams. */
+int noise_gpu_thread_release(void);
 
 /* ---- explicit device contexts --------------------------------------------
  * SURVEY 8(b) proposed noise_gpu_ctx_create(int device, ...).  The device-
@@ -348,7 +371,8 @@ int noise_gpu_decrypt_uniform_host(const uint8_t h_key[32], uint64_t nonce0,
  * context's device current for its duration and restores the caller's
  * device afterwards; it behaves exactly like the context-free function of
  * the same name.  A context is not thread-safe: one thread at a time (like
- * a CipherState).  destroy wipes and frees everything the context staged. */
+ * a CipherState).  destroy wipes and frees everything the context staged,
+ * including the descriptor path's records scratch and companion stream. */
 typedef struct noise_gpu_ctx noise_gpu_ctx;
 /* device: HIP device index (must be gfx950, else NOISE_GPU_E_NODEV) */
 int noise_gpu_ctx_create(int device, noise_gpu_ctx **out);

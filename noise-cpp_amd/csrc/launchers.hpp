@@ -24,6 +24,9 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
 
 // zero the records-path scratch of (current device, stream)
 hipError_t records_scratch_wipe(hipStream_t stream);
+// zero + free the scratch and destroy the companion stream cached for
+// (current device, stream); call before destroying `stream`
+hipError_t records_scratch_release(hipStream_t stream);
 
 bool sessions_supported(uint32_t len, const void *in, uint64_t in_stride,
                         const void *out, uint64_t out_stride);

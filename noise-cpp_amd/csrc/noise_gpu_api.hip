@@ -94,10 +94,27 @@ struct Staging {
   hipStream_t stream = nullptr;
   uint8_t *d = nullptr, *h = nullptr;
   size_t cap = 0;
-  ~Staging() {
-    if (d) (void)hipFree(d);
-    if (h) (void)hipHostFree(h);
+  ~Staging() { release(); }
+  // free everything, including the records scratch and companion stream the
+  // descriptor path cached for this staging stream (records_scratch_release)
+  void release() {
+    int cur = -1;
+    if (stream && dev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != dev) (void)hipSetDevice(dev);
+    if (stream) (void)noise_amd::records_scratch_release(stream);
+    if (d) {
+      (void)hipMemset(d, 0, cap);
+      (void)hipFree(d);
+    }
+    if (h) {
+      std::memset(h, 0, cap);
+      (void)hipHostFree(h);
+    }
     if (stream) (void)hipStreamDestroy(stream);
+    if (cur >= 0 && cur != dev) (void)hipSetDevice(cur);
+    d = h = nullptr;
+    stream = nullptr;
+    cap = 0;
+    dev = -1;
   }
   // hygiene after a call: the pinned image and the device scratch
   // (hipMemsetAsync on the staging stream; a later call's copies queue after it)
@@ -110,9 +127,8 @@ struct Staging {
     int cur = 0;
     HIP_TRY(hipGetDevice(&cur));
     if (cur != dev) {  // device switched: drop the old device's resources
-      if (d) (void)hipFree(d);
-      if (stream) (void)hipStreamDestroy(stream);
-      d = nullptr; stream = nullptr; cap = 0; dev = cur;
+      release();
+      dev = cur;
       HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     }
     if (bytes <= cap) return NOISE_GPU_OK;
@@ -158,12 +174,18 @@ struct OneCtx {
   uint8_t *d = nullptr;  // device view of the same memory
   size_t cap = 0;
   uint32_t seq = 0;
-  ~OneCtx() {
+  ~OneCtx() { release(); }
+  void release() {
+    if (stream) (void)hipStreamSynchronize(stream);
     if (h) {
       std::memset(h, 0, cap);
       (void)hipHostFree(h);
     }
     if (stream) (void)hipStreamDestroy(stream);
+    h = d = nullptr;
+    stream = nullptr;
+    cap = 0;
+    dev = -1;
   }
   int reserve(size_t bytes) {
     int cur = 0;
@@ -674,6 +696,8 @@ static int uniform_host(bool decrypt, const uint8_t h_key[32], uint64_t nonce0,
                          nrec);
   if (rc) return rc;
   if (h_in == h_out) return arg_fail("host batches must be out-of-place");
+  if (len > NOISE_GPU_UNIFORM_HOST_MAX_LEN)
+    return arg_fail("record longer than NOISE_GPU_UNIFORM_HOST_MAX_LEN for the host pipeline");
   if (nrec == 0) {
     if (seconds) *seconds = 0;
     return NOISE_GPU_OK;
@@ -686,6 +710,8 @@ static int uniform_host(bool decrypt, const uint8_t h_key[32], uint64_t nonce0,
   const uint64_t in_rec = decrypt ? (uint64_t)len + 16 : len;
   const uint64_t out_rec = decrypt ? len : (uint64_t)len + 16;
   // device chunks are packed (stride = record size), ~32 MiB of in + out
+  static_assert(2ull * NOISE_GPU_UNIFORM_HOST_MAX_LEN + 17 <= PipeCtx::kChunk,
+                "a chunk holds at least one record of the documented maximum");
   const uint64_t per = std::max<uint64_t>(1, PipeCtx::kChunk / (in_rec + out_rec + 1));
   if (per * (in_rec + out_rec) + per > PipeCtx::kChunk + (PipeCtx::kChunk >> 4))
     return arg_fail("record too large for the host pipeline");
@@ -793,6 +819,18 @@ struct CtxScope {
   } while (0)
 
 extern "C" {
+
+int noise_gpu_thread_release(void) {
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  for (int i = 0; i < kMaxCtxDev; ++i) {
+    g_stage_tab[i].release();
+    g_one_tab[i].release();
+    g_pipe_tab[i].release();
+  }
+  if (prev >= 0) (void)hipSetDevice(prev);
+  return NOISE_GPU_OK;
+}
 
 int noise_gpu_ctx_create(int device, noise_gpu_ctx **out) {
   if (!out) return arg_fail("null output pointer");

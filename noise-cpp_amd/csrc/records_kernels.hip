@@ -847,6 +847,39 @@ hipError_t records_scratch_wipe(hipStream_t stream) {
   return hipMemsetAsync(ptr, 0, size, stream);
 }
 
+// Release everything cached for (current device, stream): the scratch is
+// zeroed and freed, the companion stream and its events destroyed.  Called
+// before a stream the engine owns is destroyed (noise_gpu_ctx_destroy,
+// per-thread staging teardown), so neither a dead stream's scratch nor its
+// companion outlives it.  Synchronises `stream` first.
+static hipError_t aux_release(int dev, hipStream_t stream);
+hipError_t records_scratch_release(hipStream_t stream) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  e = hipStreamSynchronize(stream);
+  void *ptr = nullptr;
+  size_t size = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    for (size_t i = 0; i < g_scratch.size(); ++i)
+      if (g_scratch[i].dev == dev && g_scratch[i].stream == stream) {
+        ptr = g_scratch[i].ptr;
+        size = g_scratch[i].size;
+        g_scratch.erase(g_scratch.begin() + (std::ptrdiff_t)i);
+        break;
+      }
+  }
+  if (ptr) {
+    hipError_t e2 = hipMemset(ptr, 0, size);
+    if (e == hipSuccess) e = e2;
+    e2 = hipFree(ptr);
+    if (e == hipSuccess) e = e2;
+  }
+  const hipError_t e3 = aux_release(dev, stream);
+  return e == hipSuccess ? e3 : e;
+}
+
 static inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 static inline unsigned capped(uint64_t want, uint64_t cap) {
   if (want == 0) want = 1;
@@ -861,19 +894,22 @@ struct AuxStream {
   hipStream_t aux = nullptr;
   hipEvent_t fork = nullptr, prep = nullptr, join = nullptr;
 };
+struct AuxEntry {
+  int dev;
+  hipStream_t stream;
+  AuxStream a;
+};
+static std::mutex g_aux_mu;
+static std::vector<AuxEntry> g_aux;
+
 static hipError_t aux_get(AuxStream *out, hipStream_t stream) {
-  struct Entry {
-    int dev;
-    hipStream_t stream;
-    AuxStream a;
-  };
-  static std::mutex mu;
-  static std::vector<Entry> cache;
+  auto &mu = g_aux_mu;
+  auto &cache = g_aux;
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
   std::lock_guard<std::mutex> lk(mu);
-  for (const Entry &en : cache)
+  for (const AuxEntry &en : cache)
     if (en.dev == dev && en.stream == stream) {
       *out = en.a;
       return hipSuccess;
@@ -886,6 +922,30 @@ static hipError_t aux_get(AuxStream *out, hipStream_t stream) {
   cache.push_back({dev, stream, a});
   *out = a;
   return hipSuccess;
+}
+
+static hipError_t aux_release(int dev, hipStream_t stream) {
+  AuxStream a;
+  bool found = false;
+  {
+    std::lock_guard<std::mutex> lk(g_aux_mu);
+    for (size_t i = 0; i < g_aux.size(); ++i)
+      if (g_aux[i].dev == dev && g_aux[i].stream == stream) {
+        a = g_aux[i].a;
+        g_aux.erase(g_aux.begin() + (std::ptrdiff_t)i);
+        found = true;
+        break;
+      }
+  }
+  if (!found) return hipSuccess;
+  hipError_t e = hipStreamSynchronize(a.aux);
+  hipError_t e2 = hipStreamDestroy(a.aux);
+  if (e == hipSuccess) e = e2;
+  for (hipEvent_t ev : {a.fork, a.prep, a.join}) {
+    e2 = hipEventDestroy(ev);
+    if (e == hipSuccess) e = e2;
+  }
+  return e;
 }
 
 // After the classifier, two branches:

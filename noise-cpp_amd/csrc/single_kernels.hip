@@ -30,6 +30,8 @@
 //   in       L bytes (plaintext / ciphertext), zero padded to 16
 //   tag      16 bytes (decrypt: the received tag)
 //   out      ciphertext padded to 16 + tag (encrypt) / plaintext (decrypt)
+#include <mutex>
+
 #include "chachapoly_device.hpp"
 #include "launchers.hpp"
 
@@ -268,6 +270,8 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_one(const OneArgs a) {
   if (t == 0) __hip_atomic_store(hdr, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+constexpr int kMaxAttrDev = 64;
+
 size_t one_lds_bytes(uint32_t ad_len, uint32_t len) {
   const uint32_t na = (ad_len + 15u) >> 4, nl = (len + 15u) >> 4;
   return 16ull * (na + nl + 4u + 8u);
@@ -276,17 +280,24 @@ size_t one_lds_bytes(uint32_t ad_len, uint32_t len) {
 hipError_t launch_aead_one(bool decrypt, const uint32_t key[8], uint64_t nonce,
                            uint8_t *d_base, uint32_t len, uint32_t ad_len, uint32_t seq,
                            hipStream_t stream) {
-  static bool attr_set = false;  // > 64 KiB of dynamic LDS needs the opt-in
-  if (!attr_set) {
+  // > 64 KiB of dynamic LDS needs the opt-in, which is per device: set once
+  // per device, race-free across threads
+  static std::once_flag attr_once[kMaxAttrDev];
+  static hipError_t attr_err[kMaxAttrDev];
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= kMaxAttrDev) return hipErrorInvalidDevice;
+  std::call_once(attr_once[dev], [dev] {
     const int max_lds = (int)one_lds_bytes(kOneMaxAd, 65535u);
-    hipError_t e = hipFuncSetAttribute((const void *)k_aead_one<false>,
+    hipError_t r = hipFuncSetAttribute((const void *)k_aead_one<false>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, max_lds);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void *)k_aead_one<true>,
+    if (r == hipSuccess)
+      r = hipFuncSetAttribute((const void *)k_aead_one<true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, max_lds);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
+    attr_err[dev] = r;
+  });
+  if (attr_err[dev] != hipSuccess) return attr_err[dev];
   OneArgs a;
   for (int i = 0; i < 8; ++i) a.key.w[i] = key[i];
   a.nonce = nonce;

@@ -68,7 +68,9 @@ def test_host_entry_points_emulated_and_wiped():
                        timeout=900)
     if r.returncode != 0:
         pytest.fail("emulation build failed:\n" + r.stdout[-2000:] + r.stderr[-4000:])
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
+    # leak detection on: noise_gpu_ctx_destroy and noise_gpu_thread_release
+    # must free everything the engine allocated (the run ends with both)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1")
     r = subprocess.run([os.path.join(EMU, "build", "emu_api")], capture_output=True, text=True,
                        timeout=900, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]

@@ -161,6 +161,7 @@ int main() {
   }
   // ---- explicit device context: same results through its own staging
   {
+    const size_t live0 = emu::allocations().size();  // the thread's own contexts
     noise_gpu_ctx *ctx = nullptr;
     CHECK(noise_gpu_ctx_create(0, &ctx) == NOISE_GPU_OK && ctx, "ctx_create");
     CHECK(noise_gpu_ctx_destroy(ctx) == NOISE_GPU_OK, "ctx_destroy");
@@ -203,10 +204,41 @@ int main() {
       CHECK(rc == NOISE_GPU_OK && back == pt, "ctx decrypt_uniform_host rc=%d", rc);
       scan("ctx decrypt_uniform_host");
     }
+    {  // a classified descriptor batch: records scratch + companion stream on the ctx's stream
+      const uint32_t nrec = 300, L = 2100;
+      const auto pt = rbytes((size_t)nrec * 2112);
+      std::vector<noise_gpu_record> recs(nrec);
+      for (uint32_t i = 0; i < nrec; ++i)
+        recs[i] = noise_gpu_record{2112ull * i, 2128ull * i, i, 0, L, 0, 0, 0};
+      std::vector<uint8_t> out((size_t)nrec * 2128);
+      ++calls;
+      const int rc = noise_gpu_ctx_encrypt_records_host(ctx, key, 1, recs.data(), nrec, pt.data(),
+                                                        pt.size(), out.data(), out.size(), nullptr, 0);
+      std::vector<uint8_t> w(L + 16);
+      oracle_noise_encrypt(key, nrec - 1, nullptr, 0, pt.data() + 2112ull * (nrec - 1), L, w.data());
+      CHECK(rc == NOISE_GPU_OK && std::memcmp(out.data() + 2128ull * (nrec - 1), w.data(), L + 16) == 0,
+            "ctx encrypt_records_host rc=%d", rc);
+      scan("ctx encrypt_records_host");
+    }
     CHECK(noise_gpu_ctx_destroy(ctx) == NOISE_GPU_OK, "ctx_destroy");
+    // destroy freed everything the context allocated, records scratch included
+    CHECK(emu::allocations().size() == live0, "ctx_destroy left %zu allocations",
+          emu::allocations().size() - live0);
     CHECK(noise_gpu_ctx_encrypt_host(nullptr, key, 0, nullptr, 0, nullptr, 0) == NOISE_GPU_E_ARG,
           "null ctx");
   }
+  // the documented maximum of the host uniform pipeline is refused above it
+  {
+    std::vector<uint8_t> a(64), b(64);
+    double secs = 0;
+    CHECK(noise_gpu_encrypt_uniform_host(key, 0, a.data(), NOISE_GPU_UNIFORM_HOST_MAX_LEN + 16, b.data(),
+                                         NOISE_GPU_UNIFORM_HOST_MAX_LEN + 32,
+                                         NOISE_GPU_UNIFORM_HOST_MAX_LEN + 16, 1, &secs) == NOISE_GPU_E_ARG,
+          "uniform_host above the maximum length");
+  }
+  // every per-thread context released: nothing the engine allocated is left
+  CHECK(noise_gpu_thread_release() == NOISE_GPU_OK, "thread_release");
+  CHECK(emu::allocations().empty(), "thread_release left %zu allocations", emu::allocations().size());
   if (fails) {
     std::printf("emu_api FAIL (%d failures, %d calls, %d scans)\n", fails, calls, scans);
     return 1;

@@ -234,9 +234,10 @@ inline unsigned long long atomicMin(unsigned long long *p, unsigned long long v)
 
 inline hipError_t hipGetLastError() { return hipSuccess; }
 // launches run synchronously in program order: streams and events are no-ops
+// distinct handles per stream (the engine keys caches by stream), never reused
 inline hipError_t hipStreamCreateWithFlags(hipStream_t *s, unsigned) {
-  static int tag;
-  *s = &tag;
+  static std::atomic<uintptr_t> next{0x5000};
+  *s = reinterpret_cast<hipStream_t>(next.fetch_add(16));
   return hipSuccess;
 }
 inline hipError_t hipEventCreateWithFlags(hipEvent_t *e, unsigned) {

@@ -176,59 +176,112 @@ def pmc_kernels(prof, names):
 
 
 # ---------------------------------------------------------------- cpu leg
-def cpu_baseline(threads=None):
-    """Reference monocypher.c (oracle/_ref, the reference's own source built
-    by oracle/Makefile) -- or the build's C restatement if _ref is absent --
-    on this host's cores, BASELINE.md section 3: 1 KiB records, encrypt and
-    decrypt separately, at 1 thread and at the GPU's host CPU share, plus a
-    1 -> N thread encrypt line.  A bounded sample: 2^15 records per pass,
-    repeated until each figure has ~0.4-1.5 s of wall time (~15 s in all)."""
+def cpu_sample(cfg, orc, nbytes):
+    """A bounded sample of config `cfg`'s own records (same seeds, shapes and
+    nonces as make_workload, rank 0), about `nbytes` of plaintext, as a
+    descriptor batch: (key table, descriptors, plaintext, ct buffer size,
+    description)."""
+    import numpy as np
+    rd = noise_amd.record_dtype()
+    if cfg in (2, 5):
+        L = 1024 if cfg == 2 else 4096
+        R = max(64, nbytes // L)
+        lens = np.full(R, L, dtype=np.uint64)
+        keys = np.frombuffer(KEY, dtype=np.uint8).copy()
+        kidx = np.zeros(R, dtype=np.uint32)
+        nonce = np.arange(R, dtype=np.uint64)
+        what = "%d x %d B records, one key, nonces 0.." % (R, L)
+    elif cfg == 3:
+        S, L = 65536, 1024
+        R = max(64, nbytes // L)
+        i = np.arange(R, dtype=np.uint64)
+        lens = np.full(R, L, dtype=np.uint64)
+        keys = np.frombuffer(orc.synthetic(S * 32, 0x4B4559), dtype=np.uint8).copy()
+        kidx = (i % np.uint64(S)).astype(np.uint32)
+        nonce = ((i % np.uint64(S)) << np.uint64(32)) + i // np.uint64(S)
+        what = ("the first %d records of the 65536-session x 16 batch (record i: session i mod "
+                "65536, nonce (s << 32) + i div 65536), 1 KiB" % R)
+    elif cfg == 4:
+        allr = zipf_lengths(1 << 20)
+        csum = np.cumsum(allr)
+        R = int(max(64, np.searchsorted(csum, nbytes)))
+        lens = allr[:R]
+        keys = np.frombuffer(KEY, dtype=np.uint8).copy()
+        kidx = np.zeros(R, dtype=np.uint32)
+        nonce = np.arange(R, dtype=np.uint64)
+        what = ("the first %d records of the Zipf batch (64 B .. 65519 B, mean %d B), one key"
+                % (R, int(lens.sum() // R)))
+    else:
+        raise ValueError(cfg)
+    in_sz = (lens + np.uint64(15)) // np.uint64(16) * np.uint64(16)
+    ct_sz = (lens + np.uint64(31)) // np.uint64(16) * np.uint64(16)
+    d = np.zeros(R, dtype=rd)
+    d["in_off"] = np.concatenate([[0], np.cumsum(in_sz)[:-1]]).astype(np.uint64)
+    d["out_off"] = np.concatenate([[0], np.cumsum(ct_sz)[:-1]]).astype(np.uint64)
+    d["nonce"], d["len"], d["key_idx"] = nonce, lens, kidx
+    pt = np.frombuffer(orc.synthetic(int(in_sz.sum()), SEED), dtype=np.uint8).copy()
+    return keys, d, pt, int(ct_sz.sum()), int(lens.sum()), what
+
+
+def cpu_baseline(cfg=2):
+    """The reference's own monocypher.c (oracle/_ref: the reference source
+    built by oracle/Makefile, with the noise::encrypt / decrypt nonce framing
+    of noise.cpp:202-281) -- or the build's C restatement if _ref is absent --
+    on this host's cores, BASELINE.md section 3: a bounded sample of this
+    config's own records (cpu_sample), one noise::encrypt / decrypt call per
+    record, encrypt and decrypt timed separately at 1 thread, at the GPU's
+    host CPU share (16) and at nproc threads, plus a 1 -> 16 thread encrypt
+    line.  Each figure repeats whole passes over the sample until it has
+    >= 0.5-1 s of wall time (~8 s in all)."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
     orc = oracle_lib.Oracle()
     ncpu = os.cpu_count() or 1
-    threads = threads or min(SHARE_CPUS, ncpu)
-    L, R = 1024, 1 << 15
-    pt = np.frombuffer(orc.synthetic(R * L, SEED), dtype=np.uint8).copy()
-    ct = np.zeros(R * (L + 16), dtype=np.uint8)
-    back = np.zeros(R * L, dtype=np.uint8)
+    share = min(SHARE_CPUS, ncpu)
+    keys, desc, pt, ct_bytes, pt_bytes, what = cpu_sample(cfg, orc, 256 << 20)
+    R = len(desc)
+    ct = np.zeros(ct_bytes, dtype=np.uint8)
+    back = np.zeros(len(pt), dtype=np.uint8)
+    ddesc = desc.copy()
+    ddesc["in_off"], ddesc["out_off"] = desc["out_off"], desc["in_off"]
     kind = "reference" if orc.ref is not None else "port"
+    fn = orc.ref.ref_batch_records if orc.ref is not None else orc.lib.oracle_batch_records
     fails = ctypes.c_int(0)
 
     def run(dec, nthr):
-        if orc.ref is not None:
-            if dec:
-                return orc.ref.ref_batch_uniform(1, KEY, 0, ct.ctypes.data, L + 16, back.ctypes.data,
-                                                 L, L, R, nthr, ctypes.byref(fails))
-            return orc.ref.ref_batch_uniform(0, KEY, 0, pt.ctypes.data, L, ct.ctypes.data, L + 16,
-                                             L, R, nthr, ctypes.byref(fails))
         if dec:
-            return orc.lib.oracle_batch_uniform(1, KEY, 0, ct.ctypes.data, L + 16, back.ctypes.data,
-                                                L, L, R, nthr, None)
-        return orc.lib.oracle_batch_uniform(0, KEY, 0, pt.ctypes.data, L, ct.ctypes.data, L + 16,
-                                            L, R, nthr, None)
+            return fn(1, keys.ctypes.data, ddesc.ctypes.data, R, ct.ctypes.data, back.ctypes.data,
+                      nthr, ctypes.byref(fails))
+        return fn(0, keys.ctypes.data, desc.ctypes.data, R, pt.ctypes.data, ct.ctypes.data, nthr,
+                  ctypes.byref(fails))
 
     def rate(dec, nthr, seconds):
-        run(dec, nthr)  # warm
+        run(dec, nthr)  # warm (and, for decrypt, checks the ciphertext below)
         t, passes = 0.0, 0
         while t < seconds:
             t += run(dec, nthr)
             passes += 1
-        return passes * R * L / t / GIB
+        return passes * pt_bytes / t / GIB
 
-    enc1 = rate(False, 1, 1.5)
-    dec1 = rate(True, 1, 1.5)
-    encn = rate(False, threads, 1.0)
-    decn = rate(True, threads, 1.0)
-    assert np.array_equal(pt, back) and fails.value == 0, "cpu baseline round trip failed"
+    enc, dec = {}, {}
+    for nthr, secs in ((1, 1.0), (share, 0.6), (ncpu, 0.6)):
+        if str(nthr) in enc:
+            continue
+        enc[str(nthr)] = rate(False, nthr, secs)
+        dec[str(nthr)] = rate(True, nthr, secs)
+    # the round trip of the sample is exact: every tag verified, plaintext back
+    lens = desc["len"].astype(np.int64)
+    ok = fails.value == 0
+    for i in range(0, R, max(1, R // 512)):
+        o = int(desc["in_off"][i])
+        ok = ok and np.array_equal(pt[o:o + lens[i]], back[o:o + lens[i]])
+    assert ok, "cpu baseline round trip failed"
     scaling = {}
     t = 1
-    while t <= threads:
-        scaling[str(t)] = round(enc1 if t == 1 else encn if t == threads else rate(False, t, 0.4), 3)
+    while t <= share:
+        scaling[str(t)] = round(enc[str(t)] if str(t) in enc else rate(False, t, 0.3), 3)
         t *= 2
-    if str(threads) not in scaling:
-        scaling[str(threads)] = round(encn, 3)
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -237,16 +290,24 @@ def cpu_baseline(threads=None):
                 break
     except OSError:
         pass
-    value = 2.0 / (1.0 / encn + 1.0 / decn)  # enc+dec round trip, like `value`
-    return {"value": round(value, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-            "encrypt_GiBps": {"1": round(enc1, 3), str(threads): round(encn, 3)},
-            "decrypt_GiBps": {"1": round(dec1, 3), str(threads): round(decn, 3)},
+    rt = {k: 2.0 / (1.0 / enc[k] + 1.0 / dec[k]) for k in enc}  # enc+dec round trip, like `value`
+    best = max(rt, key=lambda k: rt[k])
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = ncpu
+    return {"value": round(rt[best], 3), "unit": "GiB/s", "cores": int(best), "kind": kind,
+            "config": cfg,
+            "encrypt_GiBps": {k: round(v, 3) for k, v in enc.items()},
+            "decrypt_GiBps": {k: round(v, 3) for k, v in dec.items()},
+            "round_trip_GiBps": {k: round(v, 3) for k, v in rt.items()},
             "encrypt_thread_scaling_GiBps": scaling,
-            "cpu_model": model, "nproc": ncpu,
-            "sample": "1 KiB records, 2^15 per pass, encrypt and decrypt timed separately "
-                      "(1 thread ~1.5 s each, %d threads ~1 s each, scaling points ~0.4 s); value = "
-                      "enc+dec rate at %d threads (the GPU's host CPU share; nproc reports %d); %s"
-                      % (threads, threads, ncpu, "monocypher.c via oracle/_ref" if kind == "reference"
+            "cpu_model": model, "nproc": ncpu, "affinity_cpus": affinity, "host_share": share,
+            "sample": "%s (%.0f MiB of plaintext); one noise::encrypt / decrypt call per record, "
+                      "encrypt and decrypt timed separately at 1, %d (the GPU's host CPU share) and "
+                      "%d (nproc) threads; value = the best enc+dec round-trip rate, at %s threads; %s"
+                      % (what, pt_bytes / 2**20, share, ncpu, best,
+                         "monocypher.c via oracle/_ref" if kind == "reference"
                          else "oracle/chachapoly_oracle.c")}
 
 
@@ -671,7 +732,7 @@ def main(argv=None):
         line["note"] = "--share-device test run: the ranks split the visible GPU(s); not a scaling figure"
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.stub:
         log("cpu baseline ...")
-        line["cpu_baseline"] = cpu_baseline()
+        line["cpu_baseline"] = cpu_baseline(cfg)
     if rank == 0 and world == 1 and cfg == 2 and not args.no_config1 and not args.stub:
         log("config 1 leg ...")
         line["config1"] = config1()

@@ -283,9 +283,9 @@ double oracle_batch_uniform(int decrypt, const uint8_t key[32], uint64_t n0,
                             size_t out_stride, size_t len, uint64_t nrec,
                             int threads, int *status) {
   if (threads < 1) threads = 1;
-  if (threads > 256) threads = 256;
-  pthread_t tid[256];
-  job_t jobs[256];
+  if (threads > 1024) threads = 1024;
+  static pthread_t tid[1024];  /* one caller at a time (bench / tests) */
+  static job_t jobs[1024];
   struct timespec t0, t1;
   clock_gettime(CLOCK_MONOTONIC, &t0);
   for (int t = 0; t < threads; ++t) {
@@ -412,6 +412,64 @@ static int64_t check_threads(check_t proto, uint64_t nrec, int threads, int64_t 
   }
   if (first_bad) *first_bad = first;
   return bad;
+}
+
+/* descriptor batch on `threads` pthreads (bench.py cpu_baseline, "port"
+ * kind when oracle/_ref is absent): 64-record chunks from a shared counter;
+ * returns wall seconds, *fails = decrypt MAC failures */
+typedef struct {
+  int decrypt;
+  const uint8_t *keys;
+  const oracle_rec_t *recs;
+  uint64_t nrec;
+  const uint8_t *in;
+  uint8_t *out;
+  uint64_t *next;
+  int fails;
+} bjob_t;
+
+static void *run_bjob(void *arg) {
+  bjob_t *j = (bjob_t *)arg;
+  for (;;) {
+    const uint64_t lo = __atomic_fetch_add(j->next, 64, __ATOMIC_RELAXED);
+    if (lo >= j->nrec) break;
+    const uint64_t hi = lo + 64 < j->nrec ? lo + 64 : j->nrec;
+    for (uint64_t i = lo; i < hi; ++i) {
+      const oracle_rec_t *d = j->recs + i;
+      const uint8_t *key = j->keys + 32ull * d->key_idx;
+      if (j->decrypt)
+        j->fails += oracle_noise_decrypt(key, d->nonce, NULL, 0, j->in + d->in_off,
+                                         (size_t)d->len + 16, j->out + d->out_off) != 0;
+      else
+        oracle_noise_encrypt(key, d->nonce, NULL, 0, j->in + d->in_off, d->len,
+                             j->out + d->out_off);
+    }
+  }
+  return NULL;
+}
+
+double oracle_batch_records(int decrypt, const uint8_t *keys, const void *recs, uint64_t nrec,
+                            const uint8_t *in, uint8_t *out, int threads, int *fails) {
+  if (threads < 1) threads = 1;
+  if (threads > 1024) threads = 1024;
+  static pthread_t tid[1024];
+  static bjob_t jobs[1024];
+  uint64_t next = 0;
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  for (int t = 0; t < threads; ++t) {
+    bjob_t j = {decrypt, keys, (const oracle_rec_t *)recs, nrec, in, out, &next, 0};
+    jobs[t] = j;
+    pthread_create(&tid[t], NULL, run_bjob, &jobs[t]);
+  }
+  int f = 0;
+  for (int t = 0; t < threads; ++t) {
+    pthread_join(tid[t], NULL);
+    f += jobs[t].fails;
+  }
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  if (fails) *fails = f;
+  return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
 
 int64_t oracle_check_records(int decrypt, const uint8_t *keys, uint32_t nkeys,

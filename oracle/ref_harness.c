@@ -84,9 +84,9 @@ double ref_batch_uniform(int decrypt, const uint8_t key[32], uint64_t n0,
                          size_t out_stride, size_t len, uint64_t nrec,
                          int threads, int *fails) {
   if (threads < 1) threads = 1;
-  if (threads > 256) threads = 256;
-  pthread_t tid[256];
-  job_t jobs[256];
+  if (threads > 1024) threads = 1024;
+  static pthread_t tid[1024];
+  static job_t jobs[1024];
   struct timespec t0, t1;
   clock_gettime(CLOCK_MONOTONIC, &t0);
   for (int t = 0; t < threads; ++t) {
@@ -94,6 +94,74 @@ double ref_batch_uniform(int decrypt, const uint8_t key[32], uint64_t n0,
                nrec * t / threads, nrec * (t + 1) / threads, decrypt, 0};
     jobs[t] = j;
     pthread_create(&tid[t], NULL, run_job, &jobs[t]);
+  }
+  int f = 0;
+  for (int t = 0; t < threads; ++t) {
+    pthread_join(tid[t], NULL);
+    f += jobs[t].fails;
+  }
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  if (fails) *fails = f;
+  return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
+/* ---- descriptor batches (BASELINE configs 3 and 4 on the CPU) ------------
+ * Records in the C-ABI descriptor layout (include/noise_gpu.h
+ * noise_gpu_record: in_off, out_off, nonce, ad_off u64; len, ad_len, key_idx,
+ * reserved u32), restated here; no AD.  Each record is one noise::encrypt /
+ * noise::decrypt call (crypto_aead_init_ietf + crypto_aead_write/_read with
+ * the Noise nonce), exactly what CipherState::encrypt_with_ad does per
+ * record.  Threads take 64-record chunks from a shared counter, so mixed
+ * sizes balance. */
+typedef struct {
+  uint64_t in_off, out_off, nonce, ad_off;
+  uint32_t len, ad_len, key_idx, reserved;
+} ref_rec_t;
+
+typedef struct {
+  int decrypt;
+  const uint8_t *keys;
+  const ref_rec_t *recs;
+  uint64_t nrec;
+  const uint8_t *in;
+  uint8_t *out;
+  uint64_t *next;
+  int fails;
+} rjob_t;
+
+static void *run_rjob(void *arg) {
+  rjob_t *j = (rjob_t *)arg;
+  for (;;) {
+    const uint64_t lo = __atomic_fetch_add(j->next, 64, __ATOMIC_RELAXED);
+    if (lo >= j->nrec) break;
+    const uint64_t hi = lo + 64 < j->nrec ? lo + 64 : j->nrec;
+    for (uint64_t i = lo; i < hi; ++i) {
+      const ref_rec_t *d = j->recs + i;
+      const uint8_t *key = j->keys + 32ull * d->key_idx;
+      if (j->decrypt)
+        j->fails += ref_noise_decrypt(key, d->nonce, NULL, 0, j->in + d->in_off,
+                                      (size_t)d->len + 16, j->out + d->out_off) != 0;
+      else
+        ref_noise_encrypt(key, d->nonce, NULL, 0, j->in + d->in_off, d->len,
+                          j->out + d->out_off);
+    }
+  }
+  return NULL;
+}
+
+double ref_batch_records(int decrypt, const uint8_t *keys, const void *recs, uint64_t nrec,
+                         const uint8_t *in, uint8_t *out, int threads, int *fails) {
+  if (threads < 1) threads = 1;
+  if (threads > 1024) threads = 1024;
+  static pthread_t tid[1024];
+  static rjob_t jobs[1024];
+  uint64_t next = 0;
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  for (int t = 0; t < threads; ++t) {
+    rjob_t j = {decrypt, keys, (const ref_rec_t *)recs, nrec, in, out, &next, 0};
+    jobs[t] = j;
+    pthread_create(&tid[t], NULL, run_rjob, &jobs[t]);
   }
   int f = 0;
   for (int t = 0; t < threads; ++t) {

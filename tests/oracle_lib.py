@@ -68,6 +68,10 @@ class Oracle:
                                            ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64,
                                            ctypes.c_int, ctypes.c_void_p]
         L.oracle_batch_uniform.restype = ctypes.c_double
+        L.oracle_batch_records.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+        L.oracle_batch_records.restype = ctypes.c_double
         L.oracle_check_records.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32,
                                            ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                            ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
@@ -91,6 +95,8 @@ class Oracle:
                                             ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64,
                                             ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
             R.ref_batch_uniform.restype = ctypes.c_double
+            R.ref_batch_records.argtypes = L.oracle_batch_records.argtypes
+            R.ref_batch_records.restype = ctypes.c_double
             R.ref_xx_handshake.argtypes = [ctypes.c_char_p] * 4 + [ctypes.c_void_p] * 4
             R.ref_xx_handshake.restype = ctypes.c_int
             R.ref_xx_bench.argtypes = [ctypes.c_long, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]

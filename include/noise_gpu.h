@@ -301,6 +301,22 @@ int noise_gpu_decrypt_host(const uint8_t h_key[32], uint64_t nonce,
                            size_t ct_len);
 int noise_gpu_rekey_host(uint8_t h_key[32]);
 
+/* Resident latency mode (opt-in) for the single-record entry points above,
+ * for the calling thread on its current device.  on = 1: instead of one
+ * kernel launch per record, ONE workgroup stays on the GPU and serves the
+ * thread's records through the host-mapped staging image: the host writes
+ * the record and a request line (key, nonce, lengths) and bumps a doorbell
+ * the workgroup polls; completion is the same done word.  The workgroup
+ * leaves on its own after idle_us microseconds without a request (0 = the
+ * default, 20000; at most 10 s), is relaunched by the next request, and is
+ * stopped by on = 0, noise_gpu_thread_release, thread exit and library
+ * unload.  While it runs it holds one CU and ~74 KB of its LDS, and a
+ * device-wide synchronisation (hipDeviceSynchronize) waits for it to idle
+ * out.  Results, hygiene and error behaviour are those of the launch path.
+ * Records with more than 8192 bytes of AD or more than 65535 bytes take the
+ * staged path either way. */
+int noise_gpu_set_resident(int on, uint32_t idle_us);
+
 /* Descriptor batch between HOST buffers (synchronous): the key table
  * (nkeys x 32 B), descriptors, h_in[0..in_bytes) and h_ad[0..ad_bytes) are
  * staged to the device, the records kernel runs, h_out[0..out_bytes) (and
@@ -378,6 +394,9 @@ typedef struct noise_gpu_ctx noise_gpu_ctx;
 int noise_gpu_ctx_create(int device, noise_gpu_ctx **out);
 int noise_gpu_ctx_destroy(noise_gpu_ctx *ctx);
 int noise_gpu_ctx_device(const noise_gpu_ctx *ctx, int *device);
+/* noise_gpu_set_resident for the context's single-record path; destroy
+ * stops its resident workgroup. */
+int noise_gpu_ctx_set_resident(noise_gpu_ctx *ctx, int on, uint32_t idle_us);
 int noise_gpu_ctx_encrypt_host(noise_gpu_ctx *ctx, const uint8_t h_key[32], uint64_t nonce,
                                const uint8_t *h_ad, size_t ad_len, uint8_t *h_buf, size_t len);
 int noise_gpu_ctx_decrypt_host(noise_gpu_ctx *ctx, const uint8_t h_key[32], uint64_t nonce,

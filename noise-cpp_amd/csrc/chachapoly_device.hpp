@@ -43,6 +43,48 @@ __device__ __forceinline__ uint32_t rotl32(uint32_t x, int n) {
   a += b; d = rotl32(d ^ a, 8);           \
   c += d; b = rotl32(b ^ c, 7);
 
+// Lane i of a 4-lane quad <- lane (i + n) mod 4 of the quad (DPP quad_perm:
+// one v_mov_b32_dpp, no LDS).
+template <int N>
+__device__ __forceinline__ uint32_t quad_rot(uint32_t x) {
+  constexpr int perm = ((0 + N) & 3) | (((1 + N) & 3) << 2) | (((2 + N) & 3) << 4) |
+                       (((3 + N) & 3) << 6);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, perm, 0xf, 0xf, false);
+}
+
+// ChaCha20 block on a QUAD of lanes (the latency kernel): lane q of the quad
+// holds column q of the 4x4 state -- rows a (constant q), b (key word q),
+// c (key word 4 + q), d (word 12 + q: counter, 0, n_lo, n_hi).  A column
+// round is one quarter round per lane; the diagonal round first rotates b,
+// c, d by 1, 2, 3 lanes (DPP), so lane q works on diagonal q, then rotates
+// them back.  The dependent chain is 20 quarter rounds + 60 DPP moves instead
+// of one lane's 80 quarter rounds: ~3x lower latency for one block, the
+// same instruction count per block (monocypher.c:178-200, RFC 8439 2.3).
+// out[r] = keystream word 4r + q (after the feed-forward add).
+__device__ __forceinline__ void chacha20_quad(const uint32_t k[8], uint32_t q, uint32_t ctr,
+                                              uint32_t n_lo, uint32_t n_hi, uint32_t out[4]) {
+  uint32_t a = q == 0 ? kSigma0 : q == 1 ? kSigma1 : q == 2 ? kSigma2 : kSigma3;
+  uint32_t b = q == 0 ? k[0] : q == 1 ? k[1] : q == 2 ? k[2] : k[3];
+  uint32_t c = q == 0 ? k[4] : q == 1 ? k[5] : q == 2 ? k[6] : k[7];
+  uint32_t d = q == 0 ? ctr : q == 1 ? 0u : q == 2 ? n_lo : n_hi;
+  const uint32_t a0 = a, b0 = b, c0 = c, d0 = d;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    NOISE_QR(a, b, c, d)
+    b = quad_rot<1>(b);
+    c = quad_rot<2>(c);
+    d = quad_rot<3>(d);
+    NOISE_QR(a, b, c, d)
+    b = quad_rot<3>(b);
+    c = quad_rot<2>(c);
+    d = quad_rot<1>(d);
+  }
+  out[0] = a + a0;
+  out[1] = b + b0;
+  out[2] = c + c0;
+  out[3] = d + d0;
+}
+
 // ChaCha20 block with IETF word layout: x12 = block counter, x13 = 0 (the
 // four zero bytes of the Noise nonce), x14/x15 = lo/hi 32 bits of n.
 // ks[] receives the 16 keystream words (after the feed-forward add).
@@ -341,6 +383,18 @@ __device__ __forceinline__ void lds_dma16_v(const void *vaddr, lds_void *lds_bas
                :: "v"(vaddr), "s"((uint32_t)(uintptr_t)lds_base) : "memory", "m0");
 #else
   __builtin_amdgcn_global_load_lds(vaddr, lds_base, 16, 0, 0);
+#endif
+}
+// The same with system-scope cache bypass (sc0 sc1): for host-mapped memory
+// that the host rewrites while a resident kernel keeps running (no kernel
+// start invalidates the GPU caches between requests there; a plain load can
+// hit a stale line of the previous request).
+__device__ __forceinline__ void lds_dma16_v_sys(const void *vaddr, lds_void *lds_base) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(NOISE_DMA_BUILTIN)
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off sc0 sc1"
+               :: "v"(vaddr), "s"((uint32_t)(uintptr_t)lds_base) : "memory", "m0");
+#else
+  __builtin_amdgcn_global_load_lds(vaddr, lds_base, 16, 0, 1 | 16);
 #endif
 }
 #pragma clang diagnostic pop

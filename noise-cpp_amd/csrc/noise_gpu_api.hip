@@ -7,7 +7,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <mutex>
+#include <vector>
 #include <cstring>
 #include <new>
 #include <string>
@@ -166,7 +169,27 @@ thread_local Staging *tl_stage = nullptr;
 
 // Per-thread latency-path context (single_kernels.hip): a stream and a
 // host-mapped, coherent pinned staging image the kernel reads and writes
-// over PCIe; completion is a done word the kernel stores last.
+// over PCIe; completion is a done word the kernel stores last.  In resident
+// mode (noise_gpu_set_resident) one workgroup stays on the GPU and serves
+// requests rung through the image's request line instead of one launch per
+// record; it leaves on its own after idle_us without requests (and is
+// relaunched by the next one), on the stop word, and at teardown.
+constexpr uint32_t kResidentIdleDefaultUs = 20000;
+constexpr uint32_t kResidentIdleMaxUs = 10000000;
+struct OneCtx;
+// contexts whose resident kernel may be running (stopped at library unload;
+// never destroyed, so the unload hook can still read them)
+std::mutex &resident_mu() {
+  static std::mutex *m = new std::mutex;
+  return *m;
+}
+std::vector<OneCtx *> &resident_list() {
+  static std::vector<OneCtx *> *v = new std::vector<OneCtx *>;
+  return *v;
+}
+void resident_track(OneCtx *c, bool on);
+constexpr uint32_t kOneAliveOff = 8;  // u32 in the done line: 1 while an instance runs
+
 struct OneCtx {
   int dev = -1;
   hipStream_t stream = nullptr;
@@ -174,29 +197,49 @@ struct OneCtx {
   uint8_t *d = nullptr;  // device view of the same memory
   size_t cap = 0;
   uint32_t seq = 0;
+  bool resident = false;   // opt-in (noise_gpu_set_resident)
+  uint32_t idle_us = kResidentIdleDefaultUs;
+  bool launched = false;   // a resident instance was launched and may still run
   ~OneCtx() { release(); }
+  noise_amd::OneRing *ring() { return reinterpret_cast<noise_amd::OneRing *>(h + noise_amd::kOneRingOff); }
+  // stop word -> the instance leaves at its next poll; wait for it
+  void stop_resident() {
+    if (!launched) return;
+    volatile uint32_t *stop = &ring()->stop;
+    *stop = 1u;
+    if (stream) (void)hipStreamSynchronize(stream);
+    *stop = 0u;
+    ring()->doorbell = 0u;  // served; the next instance starts from seq anyway
+    launched = false;
+    resident_track(this, false);
+  }
   void release() {
+    int cur = -1;
+    if (stream && dev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != dev) (void)hipSetDevice(dev);
+    stop_resident();
     if (stream) (void)hipStreamSynchronize(stream);
     if (h) {
       std::memset(h, 0, cap);
       (void)hipHostFree(h);
     }
     if (stream) (void)hipStreamDestroy(stream);
+    if (cur >= 0 && cur != dev) (void)hipSetDevice(cur);
     h = d = nullptr;
     stream = nullptr;
     cap = 0;
     dev = -1;
+    seq = 0;
   }
   int reserve(size_t bytes) {
     int cur = 0;
     HIP_TRY(hipGetDevice(&cur));
     if (cur != dev) {
-      if (stream) (void)hipStreamDestroy(stream);
-      stream = nullptr;
+      release();
       dev = cur;
       HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     }
     if (bytes <= cap) return NOISE_GPU_OK;
+    stop_resident();  // a running instance holds the old image's address
     size_t want = cap ? cap : 16384;
     while (want < bytes) want *= 2;
     if (h) {
@@ -210,9 +253,19 @@ struct OneCtx {
     std::memset(h, 0, want);
     HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&d), h, 0));
     cap = want;
+    seq = 0;  // a fresh image: doorbell and done word are 0
     return NOISE_GPU_OK;
   }
-  // launch already issued with `s`: wait for the done word
+  volatile uint32_t *alive() { return reinterpret_cast<volatile uint32_t *>(h + kOneAliveOff); }
+  int launch_resident(uint32_t last) {
+    *alive() = 1u;  // the instance clears it when it leaves
+    const hipError_t e = noise_amd::launch_aead_resident(d, last, idle_us, stream);
+    if (e != hipSuccess) return hip_fail(e, "launch_aead_resident");
+    if (!launched) resident_track(this, true);
+    launched = true;
+    return NOISE_GPU_OK;
+  }
+  // launch already issued (or request rung) with `s`: wait for the done word
   int wait(uint32_t s) {
     volatile uint32_t *done = reinterpret_cast<volatile uint32_t *>(h);
     for (uint64_t spin = 0;; ++spin) {
@@ -221,6 +274,11 @@ struct OneCtx {
         const hipError_t e = hipStreamQuery(stream);
         if (e == hipSuccess) {
           if (*done == s) return NOISE_GPU_OK;
+          if (resident && launched) {  // the instance idled out before the doorbell
+            const int rc = launch_resident(s - 1u);
+            if (rc) return rc;
+            continue;
+          }
           g_last_error = "latency kernel ended without its done word";
           return NOISE_GPU_E_HIP;
         }
@@ -232,17 +290,49 @@ struct OneCtx {
 thread_local OneCtx g_one_tab[kMaxCtxDev];
 thread_local OneCtx *tl_one = nullptr;
 
-// One record through the latency kernel.  dec: in = ct (len bytes) + tag.
-// Returns the kernel's status in *st (decrypt); out receives len (+16 on
-// encrypt) bytes.  Staging is wiped after use.
+void resident_track(OneCtx *c, bool on) {
+  std::lock_guard<std::mutex> lk(resident_mu());
+  std::vector<OneCtx *> &l = resident_list();
+  auto it = std::find(l.begin(), l.end(), c);
+  if (on && it == l.end()) l.push_back(c);
+  if (!on && it != l.end()) l.erase(it);
+}
+
+// Library unload (dlclose, or process exit after the threads' own teardown
+// stopped theirs): no resident kernel may outlive the code object it runs
+// from.  No HIP calls here (the runtime may already be gone at exit): set
+// every stop word, then wait -- bounded -- for each instance's alive word.
+__attribute__((destructor)) void resident_stop_all() {
+  std::vector<OneCtx *> v;
+  {
+    std::lock_guard<std::mutex> lk(resident_mu());
+    v = resident_list();
+  }
+  for (OneCtx *c : v) {
+    volatile uint32_t *stop = &c->ring()->stop;
+    *stop = 1u;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (OneCtx *c : v)
+    while (*c->alive() != 0u &&
+           std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(500)) {
+    }
+}
+
+// One record through the latency kernel (or the resident one).  dec: in = ct
+// (len bytes) + tag.  Returns the kernel's status in *st (decrypt); out
+// receives len (+16 on encrypt) bytes.  Staging is wiped after use.
 int one_record(bool dec, const uint8_t key[32], uint64_t nonce, const uint8_t *ad, uint32_t ad_len,
                const uint8_t *in, uint32_t len, const uint8_t *tag, uint8_t *out, uint32_t *st) {
   const noise_amd::OneLayout lay = noise_amd::one_layout(ad_len, len);
   OneCtx *cp = tl_one ? tl_one : ctx_of(g_one_tab);
   if (!cp) return hip_fail(hipErrorInvalidDevice, "hipGetDevice");
-  int rc = cp->reserve(lay.total);
-  if (rc) return rc;
   OneCtx &c = *cp;
+  // resident: the image is sized for the largest request once (the running
+  // instance holds its address)
+  int rc = c.reserve(c.resident ? noise_amd::one_layout(noise_amd::kOneMaxAd, 65535u).total
+                                : lay.total);
+  if (rc) return rc;
   if (ad_len) std::memcpy(c.h + lay.ad, ad, ad_len);
   if (len) std::memcpy(c.h + lay.in, in, len);
   if (dec) std::memcpy(c.h + lay.tag, tag, 16);
@@ -250,14 +340,24 @@ int one_record(bool dec, const uint8_t key[32], uint64_t nonce, const uint8_t *a
   if (s == 0) s = c.seq = 1;
   uint32_t k[8];
   key_words(key, k);
-  const hipError_t e = noise_amd::launch_aead_one(dec, k, nonce, c.d, len, ad_len, s, c.stream);
-  std::memset(k, 0, sizeof k);
-  if (e != hipSuccess) {
-    std::memset(c.h + 64, 0, lay.total - 64);
-    return hip_fail(e, "launch_aead_one");
+  if (c.resident) {
+    volatile noise_amd::OneRing *r = c.ring();
+    for (int i = 0; i < 8; ++i) r->key[i] = k[i];
+    r->nonce = nonce;
+    // every byte of the request is written before the doorbell (x86 stores
+    // are not reordered with older stores; this orders the compiler); the
+    // doorbell carries seq, lengths and direction in one 8-byte store
+    std::atomic_thread_fence(std::memory_order_release);
+    r->doorbell = noise_amd::one_doorbell(s, len, ad_len, dec);
+    if (!c.launched) rc = c.launch_resident(s - 1u);
+  } else {
+    const hipError_t e = noise_amd::launch_aead_one(dec, k, nonce, c.d, len, ad_len, s, c.stream);
+    if (e != hipSuccess) rc = hip_fail(e, "launch_aead_one");
   }
-  rc = c.wait(s);
+  std::memset(k, 0, sizeof k);
+  if (rc == NOISE_GPU_OK) rc = c.wait(s);
   if (rc == NOISE_GPU_OK) {
+    std::atomic_thread_fence(std::memory_order_acquire);
     const uint32_t status = dec ? reinterpret_cast<volatile uint32_t *>(c.h)[1] : 0u;
     if (st) *st = status;
     if (!dec) {
@@ -267,7 +367,11 @@ int one_record(bool dec, const uint8_t key[32], uint64_t nonce, const uint8_t *a
       std::memcpy(out, c.h + lay.out, len);
     }
   }
-  std::memset(c.h + 4, 0, lay.total - 4);  // hygiene: AD, record, output, status
+  // hygiene: status, the request line (key, nonce, lengths; the doorbell and
+  // stop words stay), AD, record, output
+  std::memset(c.h + 4, 0, 4);
+  std::memset(c.h + noise_amd::kOneRingOff + 8, 0, 56);
+  std::memset(c.h + 128, 0, lay.total - 128);
   return rc;
 }
 
@@ -820,6 +924,30 @@ struct CtxScope {
 
 extern "C" {
 
+static int set_resident(OneCtx &c, int on, uint32_t idle_us) {
+  if (idle_us > kResidentIdleMaxUs) return arg_fail("idle_us above 10 s");
+  if (on) {
+    int rc = check_device();
+    if (rc) return rc;
+    c.idle_us = idle_us ? idle_us : kResidentIdleDefaultUs;
+    if (c.resident) {  // new idle time: the next instance takes it
+      c.stop_resident();
+      return NOISE_GPU_OK;
+    }
+    c.resident = true;
+    return NOISE_GPU_OK;
+  }
+  c.stop_resident();
+  c.resident = false;
+  return NOISE_GPU_OK;
+}
+
+int noise_gpu_set_resident(int on, uint32_t idle_us) {
+  OneCtx *cp = tl_one ? tl_one : ctx_of(g_one_tab);
+  if (!cp) return hip_fail(hipErrorInvalidDevice, "hipGetDevice");
+  return set_resident(*cp, on, idle_us);
+}
+
 int noise_gpu_thread_release(void) {
   int prev = -1;
   if (hipGetDevice(&prev) != hipSuccess) prev = -1;
@@ -862,6 +990,10 @@ int noise_gpu_ctx_destroy(noise_gpu_ctx *ctx) {
   delete ctx;  // the contexts wipe what they staged, then free it
   if (prev >= 0) (void)hipSetDevice(prev);
   return NOISE_GPU_OK;
+}
+
+int noise_gpu_ctx_set_resident(noise_gpu_ctx *ctx, int on, uint32_t idle_us) {
+  NOISE_CTX_CALL(ctx, set_resident(ctx->one, on, idle_us));
 }
 
 int noise_gpu_ctx_device(const noise_gpu_ctx *ctx, int *device) {

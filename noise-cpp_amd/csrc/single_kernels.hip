@@ -50,6 +50,22 @@ struct OneArgs {
   uint32_t seq;   // written to the done word last
 };
 
+// 16 bytes to the host-mapped staging image with ONE system-scope,
+// write-through store (buffer_store_dwordx4 ... sc0 sc1), emitted by the
+// compiler so its VGPR hazards and vmcnt bookkeeping stay the compiler's.
+// (An inline-asm global_store_dwordx4 sc0 sc1 lost data: the compiler reused
+// its data VGPRs before the store had read them.  Two 8-byte atomic stores
+// instead cost ~8 us per 64 KiB record over PCIe.)  Buffer-resource word 3:
+// 0x00020000, the gfx9-family raw-buffer format (as in CK).
+__device__ __forceinline__ void st_sys16(uint8_t *base, uint64_t off, u32x4 w) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const __amdgpu_buffer_rsrc_t img = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(w, img, (int)off, 0, 1 | 16);  // aux: sc0 (glc) | sc1 (scc)
+#else
+  *(g_u32x4 *)(base + off) = w;
+#endif
+}
+
 // x * y by binary exponentiation: x^e (e >= 1)
 __device__ __forceinline__ F26 pow26(F26 x, uint32_t e) {
   F26 r = x;
@@ -68,13 +84,21 @@ __device__ __forceinline__ F26 add26(const F26 &a, const F26 &b) {
   return r;
 }
 
-template <bool DECRYPT>
-__global__ __launch_bounds__(kOneBlock) void k_aead_one(const OneArgs a) {
-#if defined(NOISE_HIP_EMU)
-  uint4 *lds = reinterpret_cast<uint4 *>(emu::dyn_lds);  // tools/emu
+// One record, the whole workgroup (k_aead_one: one launch per record;
+// k_aead_resident: a resident workgroup serving a doorbell ring).
+// tools/ubench/one_timing.hip builds this file with NOISE_ONE_TIMING: thread
+// 0 stamps s_memrealtime at the phase boundaries into the done line
+#ifdef NOISE_ONE_TIMING
+#define NOISE_ONE_STAMP(i)                                                       \
+  if (threadIdx.x == 0)                                                          \
+    reinterpret_cast<uint64_t *>(a.base)[2 + (i)] = __builtin_amdgcn_s_memrealtime()
 #else
-  extern __shared__ uint4 lds[];
+#define NOISE_ONE_STAMP(i) ((void)0)
 #endif
+
+template <bool DECRYPT>
+__device__ __forceinline__ void one_body(const OneArgs &a, uint4 *lds) {
+  NOISE_ONE_STAMP(0);
   const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
   const uint32_t L = a.len, A = a.ad_len;
   const uint32_t na = (A + 15u) >> 4, nl = (L + 15u) >> 4;
@@ -95,25 +119,64 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_one(const OneArgs a) {
       const uint32_t i = i0 + lane;
       if (i < npc) {
         const uint8_t *src = base + (i < na ? lay.ad + 16ull * i : lay.in + 16ull * (i - na));
-        lds_dma16_v(src, (lds_void *)(lds + i0));
+        lds_dma16_v_sys(src, (lds_void *)(lds + i0));  // the host rewrote it: bypass caches
       }
     }
   }
 
-  // 2. keystream: block b on thread b % 256; block 0 = one-time Poly key
+  // 2. keystream; block 0 = one-time Poly key.  Records of <= 63 data
+  // blocks (4032 B): block b on the quad of threads 4b..4b+3 (chacha20_quad,
+  // a third of one lane's latency; thread 4b + q holds column q).  Longer
+  // ones: block b on thread b % 256.
   const uint32_t nlo = (uint32_t)a.nonce, nhi = (uint32_t)(a.nonce >> 32);
   const uint32_t nb = (L + 63u) >> 6;
+  const bool quad = nb < 64u;  // workgroup-uniform
   uint32_t ks[kOneMaxKsPerThread][16];
+  uint32_t kq[4] = {0u, 0u, 0u, 0u};
+  uint32_t *lds32 = reinterpret_cast<uint32_t *>(lds);
+  if (quad) {
+    // every quad runs (blocks past nb unused): no divergence around the DPP
+    chacha20_quad(a.key.w, t & 3u, t >> 2, nlo, nhi, kq);
+  } else {
 #pragma unroll
-  for (int j = 0; j < kOneMaxKsPerThread; ++j) {
-    const uint32_t b = t + (uint32_t)j * kOneBlock;
-    if (b > nb) break;
-    chacha20_block(a.key.w, b, nlo, nhi, ks[j]);
+    for (int j = 0; j < kOneMaxKsPerThread; ++j) {
+      const uint32_t b = t + (uint32_t)j * kOneBlock;
+      if (b > nb) break;
+      chacha20_block(a.key.w, b, nlo, nhi, ks[j]);
+    }
   }
+  NOISE_ONE_STAMP(1);
   wait_vmem();  // this wave's DMA has landed ...
   __syncthreads();  // ... and every other wave's
+  // quad: thread (b, q) holds keystream words 4r + q (r = 0..3) of block b,
+  // i.e. word q of pieces 4(b-1) + r; XOR word-wise in LDS
+  auto quad_xor = [&](bool to_ct) {
+    const uint32_t b = t >> 2, q = t & 3u;
+    if (b == 0 || b > nb) return;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t p = 4u * (b - 1u) + (uint32_t)r;
+      if (p >= nl) break;
+      const int nbytes = (int)(L - 16u * p - 4u * q);  // bytes of this word in the record
+      if (nbytes <= 0) {
+        if (to_ct) lds32[4u * (na + p) + q] = 0u;  // padding of the last piece: zero
+        continue;
+      }
+      const uint32_t m = nbytes >= 4 ? 0xffffffffu : (1u << (8 * nbytes)) - 1u;
+      lds32[4u * (na + p) + q] = (lds32[4u * (na + p) + q] ^ kq[r]) & m;
+    }
+  };
+  if (quad) {
+    if (t < 4u) {  // block 0: r (clamped) = row 0, s = row 1
+      const uint32_t cm = t == 0 ? 0x0fffffffu : 0x0ffffffcu;
+      lds32[4u * s_r + t] = kq[0] & cm;
+      lds32[4u * s_s + t] = kq[1];
+    }
+    if (!DECRYPT) quad_xor(true);
+  }
 #pragma unroll
   for (int j = 0; j < kOneMaxKsPerThread; ++j) {
+    if (quad) break;
     const uint32_t b = t + (uint32_t)j * kOneBlock;
     if (b > nb) break;
     if (b == 0) {
@@ -135,10 +198,28 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_one(const OneArgs a) {
   }
   __syncthreads();
 
+  NOISE_ONE_STAMP(2);
   // 3. Poly1305 tree over P = na + nl + 1 blocks
   const uint32_t P = na + nl + 1u;
   const uint32_t NW = P > 256u ? 4u : 1u;  // waves taking part
-  const uint32_t T = 64u * NW;
+  // Tree width T = 2^LT lanes: the latency is ~c Horner steps plus LT tree
+  // levels (a general product, its carry and the power squaring: ~2.2 Horner
+  // steps each), so short records use a narrow tree -- one lane for <= ~8
+  // blocks -- instead of 64 lanes and six levels.  Above 256 blocks: four
+  // full waves.
+  uint32_t LT = 6;
+  if (NW == 1) {
+    uint32_t best = ~0u;
+#pragma unroll
+    for (uint32_t l = 0; l <= 6; ++l) {
+      const uint32_t cost = ((P + (1u << l) - 1u) >> l) * 10u + l * 22u;
+      if (cost < best) {
+        best = cost;
+        LT = l;
+      }
+    }
+  }
+  const uint32_t T = NW == 1 ? (1u << LT) : 64u * NW;
   const uint32_t c = (P + T - 1u) / T;    // blocks per chunk
   const uint32_t pad = T * c - P;         // leading empty positions
   if (wave < NW) {
@@ -152,7 +233,7 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_one(const OneArgs a) {
     p.r0lo = p.r0 & 3u;
     p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0u;
     const uint32_t j = wave * 64u + lane;
-    for (uint32_t q = 0; q < c; ++q) {
+    for (uint32_t q = 0; q < (j < T ? c : 0u); ++q) {
       const uint32_t pos = j * c + q;
       if (pos < pad) continue;
       const uint32_t k = pos - pad;  // real block index
@@ -164,9 +245,9 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_one(const OneArgs a) {
       }
     }
     F26 h = to26(p.h0, p.h1, p.h2, p.h3, p.h4);
-    F26 R = pow26(to26(p.r0, p.r1, p.r2, p.r3, 0u), c);  // r^c
-#pragma unroll
-    for (int l = 0; l < 6; ++l) {
+    F26 R = to26(p.r0, p.r1, p.r2, p.r3, 0u);
+    if (LT) R = pow26(R, c);  // r^c (unused by a one-lane Horner)
+    for (uint32_t l = 0; l < LT; ++l) {  // wave-uniform trip count
       F26 right;
 #pragma unroll
       for (int i = 0; i < 5; ++i) right.a[i] = (uint32_t)__shfl_down((int)h.a[i], 1 << l);
@@ -228,17 +309,27 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_one(const OneArgs a) {
   }
   __syncthreads();
 
+  NOISE_ONE_STAMP(3);
   // 4. LDS -> staging
   uint32_t *hdr = reinterpret_cast<uint32_t *>(base);
   if (!DECRYPT) {
     for (uint32_t i = t; i <= nl; i += kOneBlock) {  // ct pieces, then the tag
       const uint4 v = lds[i < nl ? na + i : s_tag];
       const u32x4 w = {v.x, v.y, v.z, v.w};
-      *(g_u32x4 *)(base + lay.out + 16ull * i) = w;
+      st_sys16(base, lay.out + 16ull * i, w);
     }
   } else {
     const bool ok = lds[s_ok].x == 0u;
-    if (ok) {  // verified: apply the keystream held in registers, write plaintext
+    if (ok && quad) {  // verified: keystream (registers) into LDS, then pieces out
+      quad_xor(false);
+      __syncthreads();
+      for (uint32_t i = t; i < nl; i += kOneBlock) {
+        const uint4 v = lds[na + i];
+        const u32x4 w = {v.x, v.y, v.z, v.w};
+        st_sys16(base, lay.out + 16ull * i, w);
+      }
+    }
+    if (ok && !quad) {  // verified: apply the keystream held in registers, write plaintext
 #pragma unroll
       for (int j = 0; j < kOneMaxKsPerThread; ++j) {
         const uint32_t b = t + (uint32_t)j * kOneBlock;
@@ -254,20 +345,125 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_one(const OneArgs a) {
                                                 v.z ^ ks[j][4 * q + 2], v.w ^ ks[j][4 * q + 3]),
                                      nbytes);
           const u32x4 w = {o.x, o.y, o.z, o.w};
-          *(g_u32x4 *)(base + lay.out + 16ull * p) = w;
+          st_sys16(base, lay.out + 16ull * p, w);
         }
       }
     }
-    if (t == 0) hdr[1] = ok ? NOISE_GPU_REC_OK : NOISE_GPU_REC_BAD_MAC;
+    if (t == 0)
+      __hip_atomic_store(hdr + 1, ok ? NOISE_GPU_REC_OK : NOISE_GPU_REC_BAD_MAC, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  NOISE_ONE_STAMP(4);
   // 5. every store of the workgroup is visible system-wide before the done
   // word (stores -> system release -> drain -> barrier -> one flag store)
+  // Every output store above is a system-scope write-through store (sc0
+  // sc1) to the host-mapped image, so draining them (vmcnt(0)) is the whole
+  // release: no L2 write-back (buffer_wbl2, ~1.4 us) is needed before the
+  // done word (MI355X_MICROARCH.md: sc1 stores drained before the flag).
+#ifdef NOISE_ONE_SYSFENCE  // A/B (tools/ubench/one_timing): the full system release
   __threadfence_system();
+#endif
 #if defined(__HIP_DEVICE_COMPILE__)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the drain the compiler may drop
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
   __syncthreads();
+  NOISE_ONE_STAMP(5);
   if (t == 0) __hip_atomic_store(hdr, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <bool DECRYPT>
+__global__ __launch_bounds__(kOneBlock) void k_aead_one(const OneArgs a) {
+#if defined(NOISE_HIP_EMU)
+  uint4 *lds = reinterpret_cast<uint4 *>(emu::dyn_lds);  // tools/emu
+#else
+  extern __shared__ uint4 lds[];
+#endif
+  one_body<DECRYPT>(a, lds);
+}
+
+// ---- resident latency kernel (opt-in: noise_gpu_set_resident) -------------
+// One workgroup stays on the GPU and serves requests from the host-mapped
+// staging image instead of one launch per record: the host writes the AD /
+// record as above plus the request line (key, nonce, lengths, direction;
+// OneRing in launchers.hpp), then bumps the doorbell; lane 0 polls the
+// doorbell over PCIe (system-scope loads, s_sleep between polls), the
+// workgroup runs one_body and raises the done word exactly like k_aead_one.
+// Every wave leaves the loop together (the decision goes through LDS) when
+//   * the stop word is set (noise_gpu_set_resident(0), context teardown,
+//     thread exit), or
+//   * no request has arrived for `idle_ticks` of the 100 MHz s_memrealtime
+//     clock -- so the grid always drains on its own, even if the host never
+//     stops it; the host relaunches it on the next request.
+// `last` is the doorbell value already served when this instance started: a
+// request rung while an idle instance was exiting is picked up by the next.
+__global__ __launch_bounds__(kOneBlock) void k_aead_resident(uint8_t *base, uint32_t last,
+                                                             uint64_t idle_ticks) {
+#if defined(NOISE_HIP_EMU)
+  uint4 *lds = reinterpret_cast<uint4 *>(emu::dyn_lds);  // tools/emu
+#else
+  extern __shared__ uint4 lds[];
+#endif
+  __shared__ uint64_t cmd[2];
+  OneRing *ring = reinterpret_cast<OneRing *>(base + kOneRingOff);
+  uint64_t t_last = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    if (threadIdx.x == 0) {
+      uint64_t db = 0, ex = 0;
+      for (;;) {
+        db = __hip_atomic_load(&ring->doorbell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((uint32_t)db != last) break;
+        if (__hip_atomic_load(&ring->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+            __builtin_amdgcn_s_memrealtime() - t_last > idle_ticks) {
+          ex = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      cmd[0] = db;
+      cmd[1] = ex;
+    }
+    __syncthreads();
+    const uint64_t db = cmd[0], ex = cmd[1];
+    __syncthreads();  // cmd is rewritten only after every thread has read it
+    if (ex) break;
+    // the rest of the request line (nonce, key) was written before the
+    // doorbell: three 16-byte system-scope loads, all in flight together
+    u32x4 q[3];
+    {
+      const u32x4 *rq = reinterpret_cast<const u32x4 *>(reinterpret_cast<const uint8_t *>(ring) + 16);
+#if defined(__HIP_DEVICE_COMPILE__)
+      asm volatile("global_load_dwordx4 %0, %3, off sc0 sc1\n\t"
+                   "global_load_dwordx4 %1, %3, off offset:16 sc0 sc1\n\t"
+                   "global_load_dwordx4 %2, %3, off offset:32 sc0 sc1\n\t"
+                   "s_waitcnt vmcnt(0)"
+                   : "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]) : "v"(rq) : "memory");
+#else
+      for (int i = 0; i < 3; ++i) q[i] = rq[i];
+#endif
+    }
+    OneArgs a;
+    a.nonce = ((uint64_t)q[0].y << 32) | q[0].x;
+    a.key.w[0] = q[1].x; a.key.w[1] = q[1].y; a.key.w[2] = q[1].z; a.key.w[3] = q[1].w;
+    a.key.w[4] = q[2].x; a.key.w[5] = q[2].y; a.key.w[6] = q[2].z; a.key.w[7] = q[2].w;
+    a.base = base;
+    a.len = (uint32_t)(db >> 32) & 0xffffu;
+    a.ad_len = (uint32_t)(db >> 48) & 0x3fffu;
+    const uint32_t dec = (uint32_t)(db >> 62) & 1u;
+    a.seq = (uint32_t)db;
+    if (a.ad_len > kOneMaxAd) a.ad_len = 0;  // the host never rings such a request
+    if (dec) one_body<true>(a, lds);
+    else one_body<false>(a, lds);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a.key.w[i] = 0u;
+    last = a.seq;
+    t_last = __builtin_amdgcn_s_memrealtime();
+  }
+  // gone: the host's unload hook waits for this word (done line, offset 8)
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(reinterpret_cast<uint32_t *>(base + 8), 0u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 constexpr int kMaxAttrDev = 64;
@@ -277,9 +473,7 @@ size_t one_lds_bytes(uint32_t ad_len, uint32_t len) {
   return 16ull * (na + nl + 4u + 8u);
 }
 
-hipError_t launch_aead_one(bool decrypt, const uint32_t key[8], uint64_t nonce,
-                           uint8_t *d_base, uint32_t len, uint32_t ad_len, uint32_t seq,
-                           hipStream_t stream) {
+static hipError_t one_attr() {
   // > 64 KiB of dynamic LDS needs the opt-in, which is per device: set once
   // per device, race-free across threads
   static std::once_flag attr_once[kMaxAttrDev];
@@ -295,9 +489,29 @@ hipError_t launch_aead_one(bool decrypt, const uint32_t key[8], uint64_t nonce,
     if (r == hipSuccess)
       r = hipFuncSetAttribute((const void *)k_aead_one<true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, max_lds);
+    if (r == hipSuccess)
+      r = hipFuncSetAttribute((const void *)k_aead_resident,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, max_lds);
     attr_err[dev] = r;
   });
-  if (attr_err[dev] != hipSuccess) return attr_err[dev];
+  return attr_err[dev];
+}
+
+hipError_t launch_aead_resident(uint8_t *d_base, uint32_t last, uint32_t idle_us,
+                                hipStream_t stream) {
+  const hipError_t e = one_attr();
+  if (e != hipSuccess) return e;
+  const size_t lds = one_lds_bytes(kOneMaxAd, 65535u);
+  hipLaunchKernelGGL(k_aead_resident, dim3(1), dim3(kOneBlock), lds, stream, d_base, last,
+                     (uint64_t)idle_us * 100ull);  // s_memrealtime: 100 MHz
+  return hipGetLastError();
+}
+
+hipError_t launch_aead_one(bool decrypt, const uint32_t key[8], uint64_t nonce,
+                           uint8_t *d_base, uint32_t len, uint32_t ad_len, uint32_t seq,
+                           hipStream_t stream) {
+  const hipError_t e0 = one_attr();
+  if (e0 != hipSuccess) return e0;
   OneArgs a;
   for (int i = 0; i < 8; ++i) a.key.w[i] = key[i];
   a.nonce = nonce;

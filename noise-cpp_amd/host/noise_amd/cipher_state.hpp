@@ -43,8 +43,10 @@ concept STLContainer = requires(T container) {
 
 class CipherState {
 private:
-  std::array<std::uint8_t, 32> k;
-  std::uint64_t n;
+  // zero-initialised (the reference leaves both indeterminate under its
+  // defaulted constructor, noise.h:101-105): a fresh CipherState has no key
+  std::array<std::uint8_t, 32> k{};
+  std::uint64_t n = 0;
 
   void encrypt_raw(const std::uint8_t *ad, std::size_t ad_len,
                    std::vector<std::uint8_t> &plaintext);

@@ -135,6 +135,9 @@ def load(path=LIB_PATH):
         "noise_gpu_ctx_decrypt_uniform_host": (ctypes.c_int, [vp, ctypes.c_char_p, u64, u8p, u64, u8p,
                                                               u64, u32, u8p, u64,
                                                               ctypes.POINTER(ctypes.c_double)]),
+        "noise_gpu_set_resident": (ctypes.c_int, [ctypes.c_int, u32]),
+        "noise_gpu_ctx_set_resident": (ctypes.c_int, [vp, ctypes.c_int, u32]),
+        "noise_gpu_thread_release": (ctypes.c_int, []),
         "noise_gpu_fill_synthetic": (ctypes.c_int, [u8p, u64, u64, u64, vp]),
         "noise_gpu_scratch_wipe": (ctypes.c_int, [vp]),
         "noise_gpu_hs_create": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, u64,
@@ -336,6 +339,16 @@ def rekey_host(key):
     buf = ctypes.create_string_buffer(_key(key), 32)
     _check(load().noise_gpu_rekey_host(buf), "noise_gpu_rekey_host")
     return buf.raw
+
+
+def set_resident(on, idle_us=0):
+    """Resident latency mode of the calling thread's single-record path
+    (noise_gpu_set_resident): one workgroup stays on the GPU while on."""
+    _check(load().noise_gpu_set_resident(1 if on else 0, idle_us), "noise_gpu_set_resident")
+
+
+def thread_release():
+    _check(load().noise_gpu_thread_release(), "noise_gpu_thread_release")
 
 
 def version():

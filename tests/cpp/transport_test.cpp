@@ -509,6 +509,7 @@ int main(int argc, char **argv) {
   // batch objects instead of producing unkeyed "ciphertext" 
   {
     noise::CipherState nokey;
+    nokey.initialize_key(std::array<std::uint8_t, 32>{});  // explicitly all zero
     for (int which = 0; which < 2; ++which) {
       threw = false;
       try {

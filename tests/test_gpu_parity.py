@@ -138,10 +138,10 @@ def test_kats_and_rekey(oracle):
 
 
 LENGTHS = [0, 1, 3, 15, 16, 17, 31, 32, 48, 63, 64, 65, 100, 127, 128, 129, 192, 255, 256, 512,
-           1000, 1023, 1024, 1025, 1040, 2048, 4096, 65519]
+           1000, 1023, 1024, 1025, 1040, 2048, 4096, 8192, 16384, 65519]
 
 # lengths served by the LDS-staged tile kernel (tile_kernel.hpp)
-TILE_LENGTHS = [64, 128, 192, 256, 512, 1024, 2048, 4096]
+TILE_LENGTHS = [64, 128, 192, 256, 512, 1024, 2048, 4096, 8192, 16384]
 
 
 @pytest.mark.parametrize("length", TILE_LENGTHS)
@@ -180,7 +180,7 @@ def test_tile_kernel_shapes(oracle, length, nrec, in_place):
 @pytest.mark.parametrize("layout", ["packed16", "odd"])
 def test_uniform_lengths_vs_oracle(oracle, length, layout):
     rng = random.Random(length * 31 + len(layout))
-    nrec = 37 if length <= 4096 else 5
+    nrec = 37 if length <= 16384 else 5
     key = rng.randbytes(32)
     n0 = rng.getrandbits(64)
     if layout == "packed16":
@@ -428,6 +428,58 @@ def test_device_context_api(oracle, golden):
         assert lib.noise_gpu_ctx_destroy(h) == 0
 
 
+def test_resident_latency_path(oracle, golden):
+    """noise_gpu_set_resident: single records served by a resident workgroup
+    polling a doorbell (single_kernels.hip k_aead_resident) -- golden records,
+    every size regime with and without AD, tampering (E_MAC, buffer left as
+    it was), the idle exit and relaunch, the explicit stop, and the launch
+    path afterwards.  Bit-exact vs the oracle / golden fixtures."""
+    import time
+    noise_amd.set_resident(True, 50000)
+    try:
+        for r in golden["transport"][::9] + golden["handshake"][::13]:
+            assert noise_amd.encrypt_host(r["key"], r["nonce"], r["ad"], r["pt"]) == r["ct"]
+            assert noise_amd.decrypt_host(r["key"], r["nonce"], r["ad"], r["ct"]) == r["pt"]
+        rng = random.Random(31)
+        key = rng.randbytes(32)
+        for length in (0, 1, 16, 17, 1024, 4096, 16384, 65519, 65535, 70000):
+            for ad_len in (0, 64, 9000):
+                if ad_len == 9000 and length > 20000:
+                    continue
+                n = rng.getrandbits(64) % (2**64 - 2)
+                ad, pt = rng.randbytes(ad_len), rng.randbytes(length)
+                ct = noise_amd.encrypt_host(key, n, ad, pt)
+                assert ct == oracle.encrypt(key, n, ad, pt), (length, ad_len)
+                assert noise_amd.decrypt_host(key, n, ad, ct) == pt
+                bad = bytearray(ct)
+                bad[rng.randrange(len(bad))] ^= 8
+                with pytest.raises(noise_amd.NoiseGpuError) as e:
+                    noise_amd.decrypt_host(key, n, ad, bytes(bad))
+                assert e.value.code == noise_amd.E_MAC
+        # a short idle time: the workgroup leaves between calls and the next
+        # request relaunches it
+        noise_amd.set_resident(True, 1000)
+        for i in range(5):
+            pt = rng.randbytes(1000)
+            assert noise_amd.encrypt_host(key, i, b"", pt) == oracle.encrypt(key, i, b"", pt)
+            time.sleep(0.01)
+    finally:
+        noise_amd.set_resident(False)
+    pt = rng.randbytes(333)
+    assert noise_amd.encrypt_host(key, 7, b"", pt) == oracle.encrypt(key, 7, b"", pt)
+    # a context in resident mode, destroyed while its workgroup runs
+    import ctypes
+    lib = noise_amd.load()
+    h = ctypes.c_void_p()
+    assert lib.noise_gpu_ctx_create(0, ctypes.byref(h)) == 0
+    assert lib.noise_gpu_ctx_set_resident(h, 1, 0) == 0
+    buf = ctypes.create_string_buffer(pt, len(pt) + 16)
+    assert lib.noise_gpu_ctx_encrypt_host(h, key, 9, None, 0, buf, len(pt)) == 0
+    assert buf.raw == oracle.encrypt(key, 9, b"", pt)
+    assert lib.noise_gpu_ctx_destroy(h) == 0
+    torch.cuda.synchronize()  # nothing left running on the device
+
+
 def test_cipherstate_cpp_surface():
     """The drop-in noise::CipherState (C++20) on the golden records."""
     exe = os.path.join(noise_amd.ROOT, "noise-cpp_amd", "bin", "cipherstate_test")
@@ -459,6 +511,21 @@ def test_xx_loopback_config1_shape():
                        timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert '"ok": true' in r.stdout
+
+
+def test_config1_bench_resident():
+    """BASELINE config 1 through the drop-in classes with the resident latency
+    workgroup (tools/config1_bench.cpp resident): XX handshake + 1000 x 1 KiB
+    records each way, round trip exact, then the explicit stop and a
+    launch-path record after it."""
+    import json
+    exe = os.path.join(noise_amd.ROOT, "noise-cpp_amd", "bin", "config1_bench")
+    r = subprocess.run([exe, "1000", "1024", "resident"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["ok"] and line["mode"] == "resident" and line["stopped"]
+    print("config1 resident:", json.dumps(line["per_record"]), json.dumps(line["latency_by_size"]))
 
 
 @pytest.mark.parametrize("sessions,messages,seed", [(100, 1000, 1), (300, 5000, 2)])

@@ -7,7 +7,11 @@
 // AEAD runs on the GPU (noise-cpp_amd/lib/libnoise_amd.so); bench.py times
 // the reference's Monocypher beside it (oracle/_ref) in the same run.
 //
-//   config1_bench <records> <len>     -> one JSON line on stdout
+//   config1_bench <records> <len> [resident]   -> one JSON line on stdout
+//
+// "resident": the single-record calls go through the resident latency
+// workgroup (noise_gpu_set_resident) instead of one kernel launch each; it is
+// switched off again at the end (the shutdown path), reported as "stopped".
 //
 // Also reported: the same records through encrypt_batch / decrypt_batch
 // (one GPU call per direction), and the per-call latency of
@@ -21,6 +25,7 @@
 #include <vector>
 
 #include "noise_amd/handshake.hpp"
+#include "noise_gpu.h"
 
 using bytes = std::vector<std::uint8_t>;
 using clk = std::chrono::steady_clock;
@@ -78,7 +83,10 @@ static std::pair<double, double> per_record(noise::CipherState &snd, noise::Ciph
 int main(int argc, char **argv) {
   const int records = argc > 1 ? std::atoi(argv[1]) : 1000;
   const int len = argc > 2 ? std::atoi(argv[2]) : 1024;
+  const bool resident = argc > 3 && std::string(argv[3]) == "resident";
   try {
+    if (resident && noise_gpu_set_resident(1, 0) != NOISE_GPU_OK)
+      throw std::runtime_error(std::string("set_resident: ") + noise_gpu_last_error());
     Pair warm;
     handshake(warm);  // device init, staging, code objects
     {
@@ -132,12 +140,21 @@ int main(int argc, char **argv) {
       lat += buf;
     }
     lat += "}";
-    std::printf("{\"handshake_ms\": %.4f, \"records\": %d, \"record_bytes\": %d, "
+    bool stopped = true;
+    if (resident) {  // shutdown path: the workgroup leaves, later calls launch again
+      stopped = noise_gpu_set_resident(0, 0) == NOISE_GPU_OK;
+      bytes m(len, 1);
+      const bytes o = m;
+      p.i_send.encrypt_with_ad(m);
+      p.r_recv.decrypt_with_ad(m);
+      stopped = stopped && m == o;
+    }
+    std::printf("{\"mode\": \"%s\", \"stopped\": %s, \"handshake_ms\": %.4f, \"records\": %d, \"record_bytes\": %d, "
                 "\"per_record\": {\"encrypt_ms\": %.3f, \"decrypt_ms\": %.3f, "
                 "\"encrypt_ms_back\": %.3f, \"decrypt_ms_back\": %.3f, \"per_record_us\": %.3f}, "
                 "\"batch\": {\"encrypt_ms\": %.3f, \"decrypt_ms\": %.3f}, "
                 "\"latency_by_size\": %s, \"ok\": true}\n",
-                hs * 1e3, records, len, e1 * 1e3, d1 * 1e3, e2 * 1e3, d2 * 1e3,
+                resident ? "resident" : "launch", stopped ? "true" : "false", hs * 1e3, records, len, e1 * 1e3, d1 * 1e3, e2 * 1e3, d2 * 1e3,
                 (e1 + d1 + e2 + d2) / 4 / records * 1e6, secs(b0, b1) * 1e3, secs(b1, b2) * 1e3,
                 lat.c_str());
   } catch (const std::exception &e) {

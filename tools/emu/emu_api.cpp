@@ -40,14 +40,15 @@ static int fails = 0, scans = 0, calls = 0;
     }                                      \
   } while (0)
 
-// every engine allocation zero (bytes [0,4) of host allocations: done word)
-static void scan(const char *after) {
+// every engine allocation zero (bytes [0,4) of host allocations: done word;
+// resident mode also leaves the alive word [8,12) and the doorbell [64,72))
+static void scan(const char *after, bool resident = false) {
   ++scans;
   std::lock_guard<std::mutex> lk(emu::alloc_mu);
   for (const auto &[p, a] : emu::allocations()) {
     const uint8_t *b = static_cast<const uint8_t *>(p);
     for (size_t i = a.host ? 4 : 0; i < a.size; ++i)
-      if (b[i]) {
+      if (b[i] && !(resident && a.host && ((i >= 8 && i < 12) || (i >= 64 && i < 72)))) {
         CHECK(false, "after %s: %s allocation of %zu bytes has byte %zu = %02x", after,
               a.host ? "host" : "device", a.size, i, b[i]);
         break;
@@ -94,6 +95,36 @@ int main() {
       CHECK(rc == NOISE_GPU_E_MAC && bad == snap, "tampered L=%zu A=%zu rc=%d", L, A, rc);
       scan("decrypt_host (tampered)");
     }
+  // ---- single records through the resident latency kernel (opt-in): the
+  // emulated launch runs it to its idle exit, so every further request is
+  // picked up by a relaunch from the host's wait loop (the lost-doorbell path)
+  CHECK(noise_gpu_set_resident(1, 300) == NOISE_GPU_OK, "set_resident on");
+  CHECK(noise_gpu_set_resident(1, 20000000) == NOISE_GPU_E_ARG, "idle above 10 s refused");
+  for (size_t L : {0ul, 17ul, 1024ul, 4096ul, 65535ul, 70000ul})
+    for (size_t A : {0ul, 64ul, 9000ul}) {
+      const uint64_t n = rng();
+      const auto pt = rbytes(L), ad = rbytes(A);
+      std::vector<uint8_t> want(L + 16), buf(pt);
+      buf.resize(L + 16);
+      oracle_noise_encrypt(key, n, ad.data(), A, pt.data(), L, want.data());
+      ++calls;
+      int rc = noise_gpu_encrypt_host(key, n, A ? ad.data() : nullptr, A, buf.data(), L);
+      CHECK(rc == NOISE_GPU_OK && buf == want, "resident encrypt_host L=%zu A=%zu rc=%d", L, A, rc);
+      scan("resident encrypt_host", true);
+      ++calls;
+      rc = noise_gpu_decrypt_host(key, n, A ? ad.data() : nullptr, A, buf.data(), L + 16);
+      CHECK(rc == NOISE_GPU_OK && std::memcmp(buf.data(), pt.data(), L) == 0,
+            "resident decrypt_host L=%zu A=%zu rc=%d", L, A, rc);
+      scan("resident decrypt_host", true);
+      std::vector<uint8_t> bad(want);
+      bad[rng() % bad.size()] ^= 0x02;
+      const std::vector<uint8_t> snap(bad);
+      ++calls;
+      rc = noise_gpu_decrypt_host(key, n, A ? ad.data() : nullptr, A, bad.data(), L + 16);
+      CHECK(rc == NOISE_GPU_E_MAC && bad == snap, "resident tampered L=%zu A=%zu rc=%d", L, A, rc);
+      scan("resident decrypt_host (tampered)", true);
+    }
+  CHECK(noise_gpu_set_resident(0, 0) == NOISE_GPU_OK, "set_resident off");
   // ---- rekey
   for (int i = 0; i < 4; ++i) {
     uint8_t k[32], w[32];
@@ -169,6 +200,7 @@ int main() {
     CHECK(noise_gpu_ctx_create(0, &ctx) == NOISE_GPU_OK && ctx, "ctx_create again");
     int dev = -1;
     CHECK(noise_gpu_ctx_device(ctx, &dev) == NOISE_GPU_OK && dev == 0, "ctx_device");
+    CHECK(noise_gpu_ctx_set_resident(ctx, 1, 200) == NOISE_GPU_OK, "ctx resident on");
     for (size_t L : {0, 17, 1024, 70000}) {
       const auto pt = rbytes(L), ad = rbytes(64);
       std::vector<uint8_t> want(L + 16), buf(pt);
@@ -177,12 +209,12 @@ int main() {
       ++calls;
       int rc = noise_gpu_ctx_encrypt_host(ctx, key, 99, ad.data(), 64, buf.data(), L);
       CHECK(rc == NOISE_GPU_OK && buf == want, "ctx encrypt_host L=%zu rc=%d", L, rc);
-      scan("ctx encrypt_host");
+      scan("ctx encrypt_host", true);
       ++calls;
       rc = noise_gpu_ctx_decrypt_host(ctx, key, 99, ad.data(), 64, buf.data(), L + 16);
       CHECK(rc == NOISE_GPU_OK && std::memcmp(buf.data(), pt.data(), L) == 0,
             "ctx decrypt_host L=%zu rc=%d", L, rc);
-      scan("ctx decrypt_host");
+      scan("ctx decrypt_host", true);
     }
     {
       const uint32_t L = 1024, R = 100;
@@ -197,12 +229,12 @@ int main() {
       CHECK(rc == NOISE_GPU_OK &&
                 std::memcmp(ct.data() + (size_t)(R - 1) * (L + 16), w.data(), L + 16) == 0,
             "ctx encrypt_uniform_host rc=%d", rc);
-      scan("ctx encrypt_uniform_host");
+      scan("ctx encrypt_uniform_host", true);
       ++calls;
       rc = noise_gpu_ctx_decrypt_uniform_host(ctx, key, 3, ct.data(), L + 16, back.data(), L, L,
                                               st.data(), R, &secs);
       CHECK(rc == NOISE_GPU_OK && back == pt, "ctx decrypt_uniform_host rc=%d", rc);
-      scan("ctx decrypt_uniform_host");
+      scan("ctx decrypt_uniform_host", true);
     }
     {  // a classified descriptor batch: records scratch + companion stream on the ctx's stream
       const uint32_t nrec = 300, L = 2100;
@@ -218,7 +250,7 @@ int main() {
       oracle_noise_encrypt(key, nrec - 1, nullptr, 0, pt.data() + 2112ull * (nrec - 1), L, w.data());
       CHECK(rc == NOISE_GPU_OK && std::memcmp(out.data() + 2128ull * (nrec - 1), w.data(), L + 16) == 0,
             "ctx encrypt_records_host rc=%d", rc);
-      scan("ctx encrypt_records_host");
+      scan("ctx encrypt_records_host", true);
     }
     CHECK(noise_gpu_ctx_destroy(ctx) == NOISE_GPU_OK, "ctx_destroy");
     // destroy freed everything the context allocated, records scratch included

@@ -14,6 +14,7 @@
 #pragma once
 #define NOISE_HIP_EMU 1
 #include <atomic>
+#include <chrono>
 #include <map>
 #include <mutex>
 #include <barrier>
@@ -173,6 +174,12 @@ void launch(K kernel, dim3 g, dim3 b, A... args) {
 #define __ATOMIC_RELAXED_ __ATOMIC_RELAXED
 #define __HIP_MEMORY_SCOPE_SYSTEM 0
 #define __hip_atomic_store(p, v, order, scope) __atomic_store_n((p), (v), __ATOMIC_SEQ_CST)
+#define __hip_atomic_load(p, order, scope) __atomic_load_n((p), __ATOMIC_SEQ_CST)
+// s_memrealtime: a 100 MHz constant clock
+#define __builtin_amdgcn_s_memrealtime()                                         \
+  ((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(              \
+       std::chrono::steady_clock::now().time_since_epoch()).count() / 10u)
+#define __builtin_amdgcn_s_sleep(n) std::this_thread::yield()
 
 #define threadIdx (emu::ctx.tid)
 #define blockIdx (emu::ctx.bid)
@@ -207,6 +214,11 @@ inline uint64_t __ballot(int p) { return emu::ballot(p != 0); }
   ((uint32_t)(c) + (uint32_t)__builtin_popcount((uint32_t)(m) &                   \
        (emu::ctx.lane < 32 ? 0u : ((1u << (emu::ctx.lane - 32)) - 1u))))
 #define __builtin_amdgcn_s_waitcnt(x) ((void)0)
+// DPP quad_perm (the only DPP control the kernels use): lane l <- lane
+// (l & ~3) | perm[l & 3]
+#define __builtin_amdgcn_mov_dpp(v, ctrl, rm, bm, bc)                            \
+  ((int)emu::shfl((uint32_t)(v), (emu::ctx.lane & ~3) |                          \
+                                     (((ctrl) >> (2 * (emu::ctx.lane & 3))) & 3)))
 #define __builtin_amdgcn_fence(...) ((void)0)
 // lanes of a real wave run in lockstep; here they meet at every wave_barrier
 // (the kernels put one after each LDS hand-off between lanes)

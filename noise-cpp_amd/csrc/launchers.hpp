@@ -47,30 +47,28 @@ constexpr uint32_t kOneMaxAd = 8192;  // larger AD takes the copy-staged path
 struct OneLayout {
   uint64_t ad, in, tag, out, total;
 };
-// [0,64) done line, GPU -> host (u32 done word, u32 status)
-// [64,128) request line of the resident kernel, host -> GPU (OneRing)
-// then AD | record | tag | output
+// Host image (host-mapped pinned):
+// [0,64) done line, GPU -> host (u32 done word, u32 status, u32 alive)
+// [64,128) OneRing: the resident kernel's stop word, host -> GPU
+// then AD | record | tag (the launch path's input) | output
 constexpr uint32_t kOneRingOff = 64;
 struct OneRing {
-  // the latest request, written last in ONE 8-byte store, so the polling
-  // lane gets the whole header in one PCIe read:
-  //   seq (bits 0..31) | len (32..47) | ad_len (48..61) | decrypt (62)
-  uint64_t doorbell;
+  uint64_t pad0;
   uint32_t stop;      // nonzero: the resident kernel exits
-  uint32_t pad0;
-  uint64_t nonce;     // 16-byte chunk 1 (with pad1)
-  uint64_t pad1;
-  uint32_t key[8];    // 16-byte chunks 2, 3
+  uint32_t pad1[13];
 };
-static_assert(sizeof(OneRing) == 64, "request line");
-__host__ __device__ inline uint64_t one_doorbell(uint32_t seq, uint32_t len, uint32_t ad_len,
-                                                 bool decrypt) {
-  return (uint64_t)seq | ((uint64_t)(len & 0xffffu) << 32) |
-         ((uint64_t)(ad_len & 0x3fffu) << 48) | ((uint64_t)decrypt << 62);
-}
-__host__ __device__ inline OneLayout one_layout(uint32_t ad_len, uint32_t len) {
+static_assert(sizeof(OneRing) == 64, "stop line");
+// Resident request image (OneReq; device memory the host writes through the
+// BAR, or host-mapped): [0,64) the request line -- four 16-byte chunks, each
+// {seq, w1, w2, w3}:
+//   chunk 0: seq, len | ad_len << 16 | decrypt << 30, nonce lo, nonce hi
+//   chunk 1: seq, key words 0, 1, 2      chunk 2: seq, key words 3, 4, 5
+//   chunk 3: seq, key words 6, 7, 0
+// then AD | record | tag at one_layout() offsets (output goes to the host
+// image).  The kernel zeroes all but the seq words after each request.
+__host__ __device__ constexpr OneLayout one_layout(uint32_t ad_len, uint32_t len) {
   const uint64_t a16 = (ad_len + 15ull) & ~15ull, l16 = (len + 15ull) & ~15ull;
-  OneLayout o;
+  OneLayout o{};
   o.ad = 128;
   o.in = o.ad + a16;
   o.tag = o.in + l16;
@@ -78,13 +76,19 @@ __host__ __device__ inline OneLayout one_layout(uint32_t ad_len, uint32_t len) {
   o.total = o.out + l16 + 16;
   return o;
 }
-size_t one_lds_bytes(uint32_t ad_len, uint32_t len);
+constexpr uint64_t kOneReqBytes = one_layout(kOneMaxAd, 65535u).total;
+// dynamic LDS of the latency kernels: staged pieces + tag, r, s, verdict and
+// the per-wave Poly1305 sums
+__host__ __device__ constexpr size_t one_lds_bytes(uint32_t ad_len, uint32_t len) {
+  return 16ull * (((ad_len + 15u) >> 4) + ((len + 15u) >> 4) + 4u + 8u);
+}
 hipError_t launch_aead_one(bool decrypt, const uint32_t key[8], uint64_t nonce,
                            uint8_t *d_base, uint32_t len, uint32_t ad_len, uint32_t seq,
                            hipStream_t stream);
-// the resident latency kernel over the staging image at d_base (sized for
-// one_layout(kOneMaxAd, 65535)); `last` = the doorbell value already served
-hipError_t launch_aead_resident(uint8_t *d_base, uint32_t last, uint32_t idle_us,
+// the resident latency kernel: requests from the image at d_req (OneReq),
+// output and done word in the host image at d_base (both sized for
+// one_layout(kOneMaxAd, 65535)); `last` = the seq already served
+hipError_t launch_aead_resident(uint8_t *d_req, uint8_t *d_base, uint32_t last, uint32_t idle_us,
                                 hipStream_t stream);
 
 hipError_t launch_x25519(const uint8_t *scalars, const uint8_t *points,

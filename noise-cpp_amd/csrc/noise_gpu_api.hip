@@ -5,10 +5,12 @@
 // every record goes through the HIP kernels, and without a gfx950 device
 // every entry point fails with NOISE_GPU_E_NODEV / NOISE_GPU_E_HIP.
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 #include <cstring>
@@ -175,6 +177,7 @@ thread_local Staging *tl_stage = nullptr;
 // record; it leaves on its own after idle_us without requests (and is
 // relaunched by the next one), on the stop word, and at teardown.
 constexpr uint32_t kResidentIdleDefaultUs = 20000;
+constexpr std::chrono::seconds kOneWaitLimit{10};
 constexpr uint32_t kResidentIdleMaxUs = 10000000;
 struct OneCtx;
 // contexts whose resident kernel may be running (stopped at library unload;
@@ -190,6 +193,21 @@ std::vector<OneCtx *> &resident_list() {
 void resident_track(OneCtx *c, bool on);
 constexpr uint32_t kOneAliveOff = 8;  // u32 in the done line: 1 while an instance runs
 
+// Where the resident kernel's request image lives (NOISE_GPU_RESIDENT_REQ,
+// read when the image is allocated): "fine" (default: fine-grained device
+// memory, which the host writes through the PCIe BAR and which stays
+// coherent with those writes -- the GPU polls local memory), or "host"
+// (host-mapped pinned memory: the GPU polls over PCIe; also the fallback when
+// fine-grained device memory cannot be allocated).  Coarse-grained device
+// memory (plain hipMalloc) is NOT an option: its lines stay valid in the
+// GPU's L2 (zeroed there by hipMemset, or left by an earlier kernel) and
+// polls served from L2 never see the host's BAR writes.
+enum ReqKind : int { kReqFine = 1, kReqHost = 2 };
+static int req_kind_env() {
+  const char *e = std::getenv("NOISE_GPU_RESIDENT_REQ");
+  return e && !std::strcmp(e, "host") ? kReqHost : kReqFine;
+}
+
 struct OneCtx {
   int dev = -1;
   hipStream_t stream = nullptr;
@@ -200,6 +218,9 @@ struct OneCtx {
   bool resident = false;   // opt-in (noise_gpu_set_resident)
   uint32_t idle_us = kResidentIdleDefaultUs;
   bool launched = false;   // a resident instance was launched and may still run
+  // resident request image (OneReq, launchers.hpp): host and device views
+  uint8_t *hreq = nullptr, *dreq = nullptr;
+  int req_kind = kReqFine;
   ~OneCtx() { release(); }
   noise_amd::OneRing *ring() { return reinterpret_cast<noise_amd::OneRing *>(h + noise_amd::kOneRingOff); }
   // stop word -> the instance leaves at its next poll; wait for it
@@ -209,15 +230,44 @@ struct OneCtx {
     *stop = 1u;
     if (stream) (void)hipStreamSynchronize(stream);
     *stop = 0u;
-    ring()->doorbell = 0u;  // served; the next instance starts from seq anyway
     launched = false;
     resident_track(this, false);
+  }
+  void release_req() {
+    if (!hreq) return;
+    if (req_kind == kReqHost) {
+      std::memset(hreq, 0, noise_amd::kOneReqBytes);
+      (void)hipHostFree(hreq);
+    } else {
+      (void)hipMemset(dreq, 0, noise_amd::kOneReqBytes);
+      (void)hipFree(dreq);
+    }
+    hreq = dreq = nullptr;
+  }
+  // the request image, zeroed (the running instance, if any, must be stopped)
+  int reserve_req() {
+    if (hreq) return NOISE_GPU_OK;
+    req_kind = req_kind_env();
+    void *p = nullptr;
+    if (req_kind == kReqFine &&
+               hipExtMallocWithFlags(&p, noise_amd::kOneReqBytes, hipDeviceMallocFinegrained) ==
+                   hipSuccess) {
+      hreq = dreq = static_cast<uint8_t *>(p);
+    } else {
+      req_kind = kReqHost;
+      HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&hreq), noise_amd::kOneReqBytes,
+                            hipHostMallocMapped | hipHostMallocCoherent));
+      HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&dreq), hreq, 0));
+    }
+    HIP_TRY(hipMemset(dreq, 0, noise_amd::kOneReqBytes));
+    return NOISE_GPU_OK;
   }
   void release() {
     int cur = -1;
     if (stream && dev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != dev) (void)hipSetDevice(dev);
     stop_resident();
     if (stream) (void)hipStreamSynchronize(stream);
+    release_req();
     if (h) {
       std::memset(h, 0, cap);
       (void)hipHostFree(h);
@@ -259,18 +309,27 @@ struct OneCtx {
   volatile uint32_t *alive() { return reinterpret_cast<volatile uint32_t *>(h + kOneAliveOff); }
   int launch_resident(uint32_t last) {
     *alive() = 1u;  // the instance clears it when it leaves
-    const hipError_t e = noise_amd::launch_aead_resident(d, last, idle_us, stream);
+    const hipError_t e = noise_amd::launch_aead_resident(dreq, d, last, idle_us, stream);
     if (e != hipSuccess) return hip_fail(e, "launch_aead_resident");
     if (!launched) resident_track(this, true);
     launched = true;
     return NOISE_GPU_OK;
   }
-  // launch already issued (or request rung) with `s`: wait for the done word
+  // launch already issued (or request rung) with `s`: wait for the done word.
+  // A record takes microseconds; no answer within kOneWaitLimit means the
+  // kernel cannot see the request (or is wedged): stop it and fail the call
+  // rather than spin for ever.
   int wait(uint32_t s) {
     volatile uint32_t *done = reinterpret_cast<volatile uint32_t *>(h);
+    const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t spin = 0;; ++spin) {
       if (*done == s) return NOISE_GPU_OK;
       if ((spin & 1023u) == 1023u) {  // now and then: has the stream failed or ended?
+        if (std::chrono::steady_clock::now() - t0 > kOneWaitLimit) {
+          if (resident) stop_resident();
+          g_last_error = "latency kernel gave no answer within 10 s";
+          return NOISE_GPU_E_HIP;
+        }
         const hipError_t e = hipStreamQuery(stream);
         if (e == hipSuccess) {
           if (*done == s) return NOISE_GPU_OK;
@@ -333,22 +392,29 @@ int one_record(bool dec, const uint8_t key[32], uint64_t nonce, const uint8_t *a
   int rc = c.reserve(c.resident ? noise_amd::one_layout(noise_amd::kOneMaxAd, 65535u).total
                                 : lay.total);
   if (rc) return rc;
-  if (ad_len) std::memcpy(c.h + lay.ad, ad, ad_len);
-  if (len) std::memcpy(c.h + lay.in, in, len);
-  if (dec) std::memcpy(c.h + lay.tag, tag, 16);
+  if (c.resident && (rc = c.reserve_req())) return rc;
+  uint8_t *img = c.resident ? c.hreq : c.h;  // where the input is staged
+  if (ad_len) std::memcpy(img + lay.ad, ad, ad_len);
+  if (len) std::memcpy(img + lay.in, in, len);
+  if (dec) std::memcpy(img + lay.tag, tag, 16);
   uint32_t s = ++c.seq;
   if (s == 0) s = c.seq = 1;
   uint32_t k[8];
   key_words(key, k);
   if (c.resident) {
-    volatile noise_amd::OneRing *r = c.ring();
-    for (int i = 0; i < 8; ++i) r->key[i] = k[i];
-    r->nonce = nonce;
-    // every byte of the request is written before the doorbell (x86 stores
-    // are not reordered with older stores; this orders the compiler); the
-    // doorbell carries seq, lengths and direction in one 8-byte store
-    std::atomic_thread_fence(std::memory_order_release);
-    r->doorbell = noise_amd::one_doorbell(s, len, ad_len, dec);
+    // the request line: four 16-byte chunks, each {seq, 3 payload words},
+    // stored whole (16-byte aligned SSE stores) after an sfence that orders
+    // them behind the staged bytes (write-combined device memory); the GPU
+    // takes the request once all four carry seq (launchers.hpp OneReq)
+    _mm_sfence();
+    const uint32_t meta = len | (ad_len << 16) | ((uint32_t)dec << 30);
+    __m128i *q = reinterpret_cast<__m128i *>(c.hreq);
+    _mm_store_si128(q + 1, _mm_setr_epi32((int)s, (int)k[0], (int)k[1], (int)k[2]));
+    _mm_store_si128(q + 2, _mm_setr_epi32((int)s, (int)k[3], (int)k[4], (int)k[5]));
+    _mm_store_si128(q + 3, _mm_setr_epi32((int)s, (int)k[6], (int)k[7], 0));
+    _mm_store_si128(q + 0, _mm_setr_epi32((int)s, (int)meta, (int)(uint32_t)nonce,
+                                          (int)(uint32_t)(nonce >> 32)));
+    _mm_sfence();
     if (!c.launched) rc = c.launch_resident(s - 1u);
   } else {
     const hipError_t e = noise_amd::launch_aead_one(dec, k, nonce, c.d, len, ad_len, s, c.stream);
@@ -367,11 +433,19 @@ int one_record(bool dec, const uint8_t key[32], uint64_t nonce, const uint8_t *a
       std::memcpy(out, c.h + lay.out, len);
     }
   }
-  // hygiene: status, the request line (key, nonce, lengths; the doorbell and
-  // stop words stay), AD, record, output
+  // hygiene: status, AD, record, output (the resident kernel zeroes its
+  // request image itself before the done word; an error path does it here)
   std::memset(c.h + 4, 0, 4);
-  std::memset(c.h + noise_amd::kOneRingOff + 8, 0, 56);
-  std::memset(c.h + 128, 0, lay.total - 128);
+  if (c.resident) {
+    std::memset(c.h + lay.out, 0, lay.total - lay.out);
+    if (rc != NOISE_GPU_OK && c.hreq) {
+      c.stop_resident();
+      if (c.req_kind == kReqHost) std::memset(c.hreq, 0, noise_amd::kOneReqBytes);
+      else (void)hipMemset(c.dreq, 0, noise_amd::kOneReqBytes);
+    }
+  } else {
+    std::memset(c.h + 128, 0, lay.total - 128);
+  }
   return rc;
 }
 
@@ -938,6 +1012,7 @@ static int set_resident(OneCtx &c, int on, uint32_t idle_us) {
     return NOISE_GPU_OK;
   }
   c.stop_resident();
+  c.release_req();  // zeroed and freed: nothing of the mode stays behind
   c.resident = false;
   return NOISE_GPU_OK;
 }

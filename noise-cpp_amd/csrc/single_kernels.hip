@@ -45,10 +45,29 @@ static_assert(kOneMaxKsPerThread == 5, "blocks per thread of a 65535-byte record
 struct OneArgs {
   KeyArg key;
   uint64_t nonce;
-  uint8_t *base;  // device-visible address of the staging image
+  uint8_t *base;        // device-visible address of the staging image (done line, output)
+  uint8_t *in_base;     // where AD / record / tag are staged: base, or the resident
+                        // kernel's request image in device memory
   uint32_t len, ad_len;
-  uint32_t seq;   // written to the done word last
+  uint32_t seq;         // written to the done word last
+  uint32_t wipe_in;     // zero the staged input (request image) before the done word
+  uint32_t staged;      // the input is already on its way into LDS (the resident
+                        // kernel's polling wave issued the DMA): only wait for it
 };
+
+// The staged input pieces [0, npc) -> LDS[0, npc) by LDS-DMA (AD pieces, then
+// record pieces and, for decrypt, the tag: contiguous in the image), by the
+// calling threads in rounds of `nthr` (64: one wave; 256: the workgroup).
+// System-scope, cache-bypassing loads: the host rewrote the image.
+__device__ __forceinline__ void one_stage_in(const uint8_t *in_base, const OneLayout &lay,
+                                             uint32_t npc, uint4 *lds, uint32_t t, uint32_t nthr) {
+  const uint32_t lane = t & 63u;
+  // wave-uniform base (readfirstlane: M0 takes an SGPR)
+  for (uint32_t i0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(t & ~63u)); i0 < npc; i0 += nthr) {
+    const uint32_t i = i0 + lane;
+    if (i < npc) lds_dma16_v_sys(in_base + lay.ad + 16ull * i, (lds_void *)(lds + i0));
+  }
+}
 
 // 16 bytes to the host-mapped staging image with ONE system-scope,
 // write-through store (buffer_store_dwordx4 ... sc0 sc1), emitted by the
@@ -84,8 +103,6 @@ __device__ __forceinline__ F26 add26(const F26 &a, const F26 &b) {
   return r;
 }
 
-// One record, the whole workgroup (k_aead_one: one launch per record;
-// k_aead_resident: a resident workgroup serving a doorbell ring).
 // tools/ubench/one_timing.hip builds this file with NOISE_ONE_TIMING: thread
 // 0 stamps s_memrealtime at the phase boundaries into the done line
 #ifdef NOISE_ONE_TIMING
@@ -95,6 +112,41 @@ __device__ __forceinline__ F26 add26(const F26 &a, const F26 &b) {
 #else
 #define NOISE_ONE_STAMP(i) ((void)0)
 #endif
+
+// Step 5 of every single-record body: the resident kernel's request image
+// is zeroed (the key words of the request line -- its sequence words stay --
+// and the npc staged input pieces), then every store of the workgroup is
+// visible system-wide before the done word (stores -> drain -> barrier -> one
+// flag store).  Every store above is a system-scope write-through store (sc0
+// sc1), so draining them (vmcnt(0)) is the whole release: no L2 write-back
+// (buffer_wbl2, ~1.4 us) is needed before the done word (MI355X_MICROARCH.md:
+// sc1 stores drained before the flag).  The zeroing must land before the
+// done word too: the host writes the next request only after it.
+__device__ __forceinline__ void one_finish(const OneArgs &a, const OneLayout &lay, uint32_t npc) {
+  const uint32_t t = threadIdx.x;
+  if (a.wipe_in) {
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    for (uint32_t i = t; i < npc; i += kOneBlock) st_sys16(a.in_base, lay.ad + 16ull * i, z);
+    if (t < 4) {
+      const u32x4 w = {a.seq, 0u, 0u, 0u};
+      st_sys16(a.in_base, 16ull * t, w);
+    }
+  }
+#ifdef NOISE_ONE_SYSFENCE  // A/B (tools/ubench/one_timing): the full system release
+  __threadfence_system();
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  __syncthreads();
+  NOISE_ONE_STAMP(5);
+  if (t == 0)
+    __hip_atomic_store(reinterpret_cast<uint32_t *>(a.base), a.seq, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// One record, the whole workgroup (k_aead_one: one launch per record;
+// k_aead_resident: a resident workgroup serving a doorbell ring).
 
 template <bool DECRYPT>
 __device__ __forceinline__ void one_body(const OneArgs &a, uint4 *lds) {
@@ -111,18 +163,7 @@ __device__ __forceinline__ void one_body(const OneArgs &a, uint4 *lds) {
   // 1. staging -> LDS by LDS-DMA: AD, record and (decrypt) tag pieces land
   // at lds[0..npc) without passing through registers, so nothing waits for
   // the PCIe round trip until the keystream blocks below are computed
-  {
-    const uint32_t npc = na + nl + (DECRYPT ? 1u : 0u);
-    // wave-uniform base (readfirstlane: M0 takes an SGPR)
-    for (uint32_t i0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(wave * 64u)); i0 < npc;
-         i0 += kOneBlock) {
-      const uint32_t i = i0 + lane;
-      if (i < npc) {
-        const uint8_t *src = base + (i < na ? lay.ad + 16ull * i : lay.in + 16ull * (i - na));
-        lds_dma16_v_sys(src, (lds_void *)(lds + i0));  // the host rewrote it: bypass caches
-      }
-    }
-  }
+  if (!a.staged) one_stage_in(a.in_base, lay, na + nl + (DECRYPT ? 1u : 0u), lds, t, kOneBlock);
 
   // 2. keystream; block 0 = one-time Poly key.  Records of <= 63 data
   // blocks (4032 B): block b on the quad of threads 4b..4b+3 (chacha20_quad,
@@ -354,21 +395,7 @@ __device__ __forceinline__ void one_body(const OneArgs &a, uint4 *lds) {
                          __HIP_MEMORY_SCOPE_SYSTEM);
   }
   NOISE_ONE_STAMP(4);
-  // 5. every store of the workgroup is visible system-wide before the done
-  // word (stores -> system release -> drain -> barrier -> one flag store)
-  // Every output store above is a system-scope write-through store (sc0
-  // sc1) to the host-mapped image, so draining them (vmcnt(0)) is the whole
-  // release: no L2 write-back (buffer_wbl2, ~1.4 us) is needed before the
-  // done word (MI355X_MICROARCH.md: sc1 stores drained before the flag).
-#ifdef NOISE_ONE_SYSFENCE  // A/B (tools/ubench/one_timing): the full system release
-  __threadfence_system();
-#endif
-#if defined(__HIP_DEVICE_COMPILE__)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-  __syncthreads();
-  NOISE_ONE_STAMP(5);
-  if (t == 0) __hip_atomic_store(hdr, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  one_finish(a, lay, na + nl + (DECRYPT ? 1u : 0u));
 }
 
 template <bool DECRYPT>
@@ -382,84 +409,438 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_one(const OneArgs a) {
 }
 
 // ---- resident latency kernel (opt-in: noise_gpu_set_resident) -------------
-// One workgroup stays on the GPU and serves requests from the host-mapped
-// staging image instead of one launch per record: the host writes the AD /
-// record as above plus the request line (key, nonce, lengths, direction;
-// OneRing in launchers.hpp), then bumps the doorbell; lane 0 polls the
-// doorbell over PCIe (system-scope loads, s_sleep between polls), the
-// workgroup runs one_body and raises the done word exactly like k_aead_one.
-// Every wave leaves the loop together (the decision goes through LDS) when
-//   * the stop word is set (noise_gpu_set_resident(0), context teardown,
-//     thread exit), or
-//   * no request has arrived for `idle_ticks` of the 100 MHz s_memrealtime
-//     clock -- so the grid always drains on its own, even if the host never
-//     stops it; the host relaunches it on the next request.
-// `last` is the doorbell value already served when this instance started: a
-// request rung while an idle instance was exiting is picked up by the next.
-__global__ __launch_bounds__(kOneBlock) void k_aead_resident(uint8_t *base, uint32_t last,
-                                                             uint64_t idle_ticks) {
+// One workgroup stays on the GPU and serves the thread's single records
+// instead of one launch per record.
+//
+//   * Requests arrive in a REQUEST IMAGE in device memory that the host
+//     writes through the PCIe BAR (write-combined stores; launchers.hpp
+//     OneReq): the AD / record / tag at one_layout() offsets, then the
+//     request line -- four 16-byte chunks {seq, three payload words}: lengths
+//     and direction, the nonce, the key.  Lanes 0..3 of wave 0 poll the four
+//     chunks (system-scope loads, local memory: ~1 us per poll instead of a
+//     PCIe round trip) and take a request when all four carry a new seq; the
+//     host stores the chunks after an sfence that follows the data, and PCIe
+//     keeps posted writes in order, so everything else has landed by then.
+//   * Output, status and the done word go to the host-mapped image (write-
+//     through stores) exactly as in the launch path; the request image is
+//     zeroed (but for the chunks' seq words) before the done word.
+//   * SPECULATION.  Noise sends consecutive nonces under one key, so after
+//     answering (key, n) the workgroup precomputes for (key, n + 1) while the
+//     host turns round: ChaCha blocks 0..63 of that nonce (one block per quad
+//     of lanes, chacha20_quad) and the Poly1305 powers r, r^2 .. r^256 (nine
+//     levels of products).  A request that matches a slot (key and nonce;
+//     two slots, least recently used replaced, for a session's send and
+//     receive keys) of <= 63 keystream blocks and <= 256 Poly1305 blocks
+//     then costs only its data load, one XOR and ONE product per 16-byte
+//     block -- sum_t m_t r^(P-t) in parallel over the 256 lanes, reduced by
+//     shuffles -- instead of the block-0 -> r -> Horner-tree chain
+//     (one_body_fast).  Anything else runs one_body.
+//   * Every wave leaves the loop together (the decision goes through LDS)
+//     when the stop word in the host image is set (polled every 32 polls), or
+//     no request has arrived for `idle_ticks` of the 100 MHz s_memrealtime
+//     clock -- so the grid always drains on its own.  On the way out the
+//     speculation slots (future keystream, key copies) are zeroed in LDS.
+// `last` is the seq already served when this instance started: a request
+// rung while an idle instance was exiting is picked up by the next one.
+constexpr uint32_t kSpecBlocks = 64;   // keystream blocks 0..63 of the next nonce
+constexpr uint32_t kSpecPowers = 256;  // r^1 .. r^256
+constexpr uint32_t kSpecSlots = 2;
+struct SpecSlot {                      // LDS, 9328 B
+  uint32_t key[8];
+  uint32_t nlo, nhi, valid, stamp;     // stamp: last use (LRU)
+  uint32_t r[4], s[4];
+  uint32_t nks;                        // keystream blocks 1..nks are speculated
+  uint32_t pad[7];
+  uint32_t ks[kSpecBlocks * 16];       // block b word w at ks[16 b + w] (b >= 1)
+  uint32_t pw[kSpecPowers * 5];        // r^e (radix 2^26) at pw[5 (e - 1)]
+};
+static_assert(sizeof(SpecSlot) % 16 == 0, "slot alignment");
+// LDS words after the slots: the request broadcast (16), the next nonce's
+// block-0 words r0..3 (clamped), s0..3 and a valid flag (9)
+constexpr uint32_t kResCmdWords = 16, kResPreWords = 16;
+
+__device__ __forceinline__ F26 pw_get(const SpecSlot *sp, uint32_t e) {
+  F26 f;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) f.a[i] = sp->pw[5u * (e - 1u) + i];
+  return f;
+}
+__device__ __forceinline__ void pw_put(SpecSlot *sp, uint32_t e, const F26 &f) {
+#pragma unroll
+  for (int i = 0; i < 5; ++i) sp->pw[5u * (e - 1u) + i] = f.a[i];
+}
+// program-order LDS hand-off within ONE wave (no workgroup barrier)
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Block 0 of (key, nonce) on the quad of threads 0..3: pre[q] = r word q
+// (clamped), pre[4 + q] = s word q, pre[8] = 1.  Called by all of wave 0
+// (every quad computes, the first one stores: no divergence around the DPP)
+// while the rest of the workgroup waits for its data.
+__device__ __forceinline__ void spec_block0(uint32_t *pre, const uint32_t key[8], uint64_t nonce,
+                                            uint32_t lane) {
+  uint32_t kq[4];
+  const uint32_t q = lane & 3u;
+  chacha20_quad(key, q, 0u, (uint32_t)nonce, (uint32_t)(nonce >> 32), kq);
+  if (lane < 4) {
+    pre[q] = kq[0] & (q == 0 ? 0x0fffffffu : 0x0ffffffcu);
+    pre[4 + q] = kq[1];
+    if (q == 0) pre[8] = 1u;
+  }
+}
+
+// Fill slot sp for (key, nonce) with keystream blocks 1..nks (nks <= 63):
+// the whole workgroup.  pre: block 0 of (key, nonce) if pre[8] is set
+// (spec_block0 ran during the request), else it is computed here first.
+//   wave 0        : the power ladder r^1..r^16 and r^32..r^256 by 16s, in
+//                   LDS with wave-level ordering only (8 levels of one
+//                   product; no workgroup barrier between them);
+//   waves 1..3    : the keystream blocks, one per quad (48 at a time);
+//   all           : r^(16a + b) = r^(16a) r^b for the rest, one product each.
+__device__ void spec_fill(SpecSlot *sp, uint32_t *pre, const uint32_t key[8], uint64_t nonce,
+                          uint32_t stamp, uint32_t nks) {
+  const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+  const uint32_t nlo = (uint32_t)nonce, nhi = (uint32_t)(nonce >> 32);
+  if (!pre[8]) {  // workgroup-uniform
+    if (wave == 0) spec_block0(pre, key, nonce, lane);
+    __syncthreads();
+  }
+  if (t == 0) sp->valid = 0u;
+  if (wave == 0) {
+    if (lane == 0) pw_put(sp, 1u, to26(pre[0], pre[1], pre[2], pre[3], 0u));
+    wave_sync_lds();
+    // r^(2^l + i) = r^(2^l) r^i, i = 1 .. 2^l: r^1 .. r^16
+#pragma unroll 1
+    for (uint32_t l = 1; l <= 8; l <<= 1) {
+      if (lane < l) pw_put(sp, l + lane + 1u, mul26(pw_get(sp, l), pw_get(sp, lane + 1u)));
+      wave_sync_lds();
+    }
+    // r^(16 (2^l + i)) = r^(16 2^l) r^(16 i): the multiples of 16 up to 256
+#pragma unroll 1
+    for (uint32_t l = 1; l <= 8; l <<= 1) {
+      if (lane < l)
+        pw_put(sp, 16u * (l + lane + 1u), mul26(pw_get(sp, 16u * l), pw_get(sp, 16u * (lane + 1u))));
+      wave_sync_lds();
+    }
+  } else {
+    const uint32_t qd = (t - 64u) >> 2, wq0 = 16u * (wave - 1u);  // 48 quads; the wave's first
+#pragma unroll 1
+    for (uint32_t b0 = 1u + wq0; b0 <= nks; b0 += 48u) {  // wave-uniform trip count
+      const uint32_t b = b0 + (qd - wq0);
+      uint32_t kq[4];
+      chacha20_quad(key, t & 3u, b, nlo, nhi, kq);
+      if (b <= nks) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sp->ks[16u * b + 4u * r + (t & 3u)] = kq[r];
+      }
+    }
+  }
+  __syncthreads();
+  {  // the rest: r^(16 a + b) = r^(16 a) r^b, a = 1..15, b = 1..15
+    const uint32_t e = t + 1u, hi = e >> 4, lo = e & 15u;
+    if (hi >= 1u && hi <= 15u && lo != 0u) pw_put(sp, e, mul26(pw_get(sp, 16u * hi), pw_get(sp, lo)));
+  }
+  if (t < 8) sp->key[t] = key[t];
+  if (t < 4) {
+    sp->r[t] = pre[t];
+    sp->s[t] = pre[4 + t];
+  }
+  if (t == 0) {
+    sp->nlo = nlo;
+    sp->nhi = nhi;
+    sp->stamp = stamp;
+    sp->nks = nks;
+  }
+  __syncthreads();
+  if (t == 0) {
+    sp->valid = 1u;
+    pre[8] = 0u;
+  }
+  __syncthreads();
+}
+
+// Sum of v over the wave (every lane holds it): two quad_perm DPP adds and
+// two row_ror DPP adds give each lane its row's sum; the four row sums come
+// out through readlane (no LDS crossbar round trips).  The caller keeps the
+// row sums below 2^32.
+__device__ __forceinline__ uint32_t row_sum_dpp(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xf, 0xf, false);  // row_ror:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false);  // row_ror:8
+  return v;
+}
+__device__ __forceinline__ uint32_t rows_total(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
+         (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+}
+
+// A speculated record: sp holds (key, nonce)'s keystream blocks 1..nks and
+// r^1..r^256; the record has <= nks keystream blocks and P = na + nl + 1 <=
+// 256 Poly1305 blocks.  Thread t < P takes block t (AD pieces, then
+// ciphertext pieces -- encrypt makes them here -- then the length block) and
+// computes (m_t + 2^128) r^(P-t); the 256 products are summed per wave by
+// DPP (radix 2^26 limbs, renormalised after 16 terms) and the four wave sums
+// by thread 0, which adds s and writes / checks the tag.  Same result as the
+// Horner chain of crypto_aead_write / crypto_aead_read (monocypher.c:2858-
+// 2929): the sum IS that polynomial evaluated at r.  While the record's data
+// is in flight, threads 0..3 compute block 0 of the next nonce (pre).
+template <bool DECRYPT>
+__device__ void one_body_fast(const OneArgs &a, uint4 *lds, const SpecSlot *sp, uint32_t *pre) {
+  const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+  const uint32_t L = a.len, A = a.ad_len;
+  const uint32_t na = (A + 15u) >> 4, nl = (L + 15u) >> 4;
+  const OneLayout lay = one_layout(A, L);
+  uint8_t *base = a.base;
+  const uint32_t s_tag = na + nl, s_ok = s_tag + 1, s_w = s_ok + 1;
+  const uint32_t npc = na + nl + (DECRYPT ? 1u : 0u);
+  // 1. request image -> LDS (one piece per thread: npc <= 257), unless the
+  // polling wave already issued it; block 0 of nonce + 1 meanwhile
+  if (!a.staged) one_stage_in(a.in_base, lay, npc, lds, t, kOneBlock);
+  if (wave == 0) spec_block0(pre, a.key.w, a.nonce + 1u, lane);
+  wait_vmem();
+  __syncthreads();
+  NOISE_ONE_STAMP(1);
+  // 2. block t: the product (m_t + 2^128) r^(P - t)
+  const uint32_t P = na + nl + 1u;
+  F26 h;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) h.a[i] = 0u;
+  if (t < P) {
+    uint4 m;
+    if (t < na) {
+      const uint32_t rem = A - 16u * t;
+      m = mask_bytes(lds[t], rem >= 16u ? 16 : (int)rem);
+    } else if (t < na + nl) {
+      const uint32_t p = t - na, rem = L - 16u * p;
+      const int nbytes = rem >= 16u ? 16 : (int)rem;
+      const uint32_t *ks = sp->ks + 16u * (1u + (p >> 2)) + 4u * (p & 3u);
+      const uint4 v = lds[na + p];
+      if (!DECRYPT) {
+        m = mask_bytes(make_uint4(v.x ^ ks[0], v.y ^ ks[1], v.z ^ ks[2], v.w ^ ks[3]), nbytes);
+        lds[na + p] = m;  // ciphertext, zero padded
+      } else {
+        m = mask_bytes(v, nbytes);
+      }
+    } else {
+      m = make_uint4(A, 0u, L, 0u);  // LE64(ad_len) || LE64(len)
+    }
+    h = mul26(to26(m.x, m.y, m.z, m.w, 1u), pw_get(sp, P - t));
+  }
+  // < 2^26 + 2^9 per term: a row's 16 terms fit in 32 bits, renormalised
+  // before the four rows are added
+#pragma unroll
+  for (int i = 0; i < 5; ++i) h.a[i] = row_sum_dpp(h.a[i]);
+  carry26(h);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) h.a[i] = rows_total(h.a[i]);
+  if (lane == 0) {
+    lds[s_w + 2 * wave] = make_uint4(h.a[0], h.a[1], h.a[2], h.a[3]);
+    lds[s_w + 2 * wave + 1] = make_uint4(h.a[4], 0u, 0u, 0u);
+  }
+  __syncthreads();
+  if (t == 0) {
+    F26 H;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) H.a[i] = 0u;
+#pragma unroll
+    for (uint32_t w = 0; w < kOneBlock / 64; ++w) {
+      const uint4 v0 = lds[s_w + 2 * w], v1 = lds[s_w + 2 * w + 1];
+      H.a[0] += v0.x; H.a[1] += v0.y; H.a[2] += v0.z; H.a[3] += v0.w; H.a[4] += v1.x;
+    }
+    carry26(H);
+    carry26(H);
+    Poly1305 p;
+    from26(H, p.h0, p.h1, p.h2, p.h3, p.h4);
+    p.s0 = sp->s[0]; p.s1 = sp->s[1]; p.s2 = sp->s[2]; p.s3 = sp->s[3];
+    uint32_t tag[4];
+    poly_final(p, tag);
+    if (!DECRYPT) {
+      lds[s_tag] = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+    } else {
+      const uint4 w = lds[s_tag];
+      lds[s_ok] = make_uint4((w.x ^ tag[0]) | (w.y ^ tag[1]) | (w.z ^ tag[2]) | (w.w ^ tag[3]), 0u,
+                             0u, 0u);
+    }
+  }
+  __syncthreads();
+  NOISE_ONE_STAMP(3);
+  // 3. LDS -> host image
+  if (!DECRYPT) {
+    if (t <= nl) {  // ct pieces, then the tag
+      const uint4 v = lds[t < nl ? na + t : s_tag];
+      const u32x4 w = {v.x, v.y, v.z, v.w};
+      st_sys16(base, lay.out + 16ull * t, w);
+    }
+  } else {
+    const bool ok = lds[s_ok].x == 0u;
+    if (ok && t < nl) {  // verified: plaintext out
+      const uint32_t rem = L - 16u * t;
+      const uint32_t *ks = sp->ks + 16u * (1u + (t >> 2)) + 4u * (t & 3u);
+      const uint4 v = lds[na + t];
+      const uint4 o = mask_bytes(make_uint4(v.x ^ ks[0], v.y ^ ks[1], v.z ^ ks[2], v.w ^ ks[3]),
+                                 rem >= 16u ? 16 : (int)rem);
+      const u32x4 w = {o.x, o.y, o.z, o.w};
+      st_sys16(base, lay.out + 16ull * t, w);
+    }
+    if (t == 0)
+      __hip_atomic_store(reinterpret_cast<uint32_t *>(base) + 1,
+                         ok ? NOISE_GPU_REC_OK : NOISE_GPU_REC_BAD_MAC, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  NOISE_ONE_STAMP(4);
+  one_finish(a, lay, npc);
+}
+
+// 16 bytes of the request image, bypassing the caches (the host rewrites it
+// through the BAR behind the GPU's back)
+__device__ __forceinline__ u32x4 ld_sys16(const uint8_t *p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
+               : "=v"(v) : "v"(p) : "memory");
+  return v;
+#else
+  const volatile uint32_t *q = reinterpret_cast<const volatile uint32_t *>(p);
+  u32x4 v = {q[0], q[1], q[2], q[3]};
+  return v;
+#endif
+}
+
+// LDS: the staging image (one_lds_bytes(kOneMaxAd, 65535)), then the
+// speculation slots, then the request broadcast and the next block 0
+size_t resident_lds_bytes();
+__global__ __launch_bounds__(kOneBlock) void k_aead_resident(uint8_t *req, uint8_t *base,
+                                                             uint32_t last, uint64_t idle_ticks) {
 #if defined(NOISE_HIP_EMU)
   uint4 *lds = reinterpret_cast<uint4 *>(emu::dyn_lds);  // tools/emu
 #else
   extern __shared__ uint4 lds[];
 #endif
-  __shared__ uint64_t cmd[2];
-  OneRing *ring = reinterpret_cast<OneRing *>(base + kOneRingOff);
+  const uint32_t t = threadIdx.x, lane = t & 63u;
+  const size_t stage = one_lds_bytes(kOneMaxAd, 65535u);
+  SpecSlot *slots = reinterpret_cast<SpecSlot *>(reinterpret_cast<uint8_t *>(lds) + stage);
+  uint32_t *cmd = reinterpret_cast<uint32_t *>(slots + kSpecSlots);
+  uint32_t *pre = cmd + kResCmdWords;
+  if (t < kSpecSlots) slots[t].valid = 0u;
+  if (t == 0) pre[8] = 0u;
+  const OneRing *ring = reinterpret_cast<const OneRing *>(base + kOneRingOff);
   uint64_t t_last = __builtin_amdgcn_s_memrealtime();
+  uint32_t stamp = 0, nks = 16u;
+  __syncthreads();
   for (;;) {
-    if (threadIdx.x == 0) {
-      uint64_t db = 0, ex = 0;
+    if (t < 64) {  // wave 0 polls; lanes 0..3 own the request line's chunks
+      uint32_t ex = 0, polls = 0;
+      u32x4 c = {0u, 0u, 0u, 0u};
       for (;;) {
-        db = __hip_atomic_load(&ring->doorbell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if ((uint32_t)db != last) break;
-        if (__hip_atomic_load(&ring->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
-            __builtin_amdgcn_s_memrealtime() - t_last > idle_ticks) {
+        if (lane < 4) c = ld_sys16(req + 16u * lane);
+        const uint32_t seq = (uint32_t)__shfl((int)c.x, 0);
+        const uint64_t same = __ballot(lane < 4 && c.x == seq);
+        if (seq != last && (same & 0xfull) == 0xfull) {
+#ifdef NOISE_ONE_TIMING
+          if (lane == 0) reinterpret_cast<uint64_t *>(base)[2] = __builtin_amdgcn_s_memrealtime();
+#endif
+          break;
+        }
+        if ((++polls & 31u) == 0u &&
+            (__hip_atomic_load(&ring->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+             __builtin_amdgcn_s_memrealtime() - t_last > idle_ticks)) {
           ex = 1;
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
       }
-      cmd[0] = db;
-      cmd[1] = ex;
+      if (!ex) {  // this wave issues the record's DMA at once (the bodies only wait for it)
+        const uint32_t meta = (uint32_t)__shfl((int)c.y, 0);
+        const uint32_t L = meta & 0xffffu, A = (meta >> 16) & 0x3fffu, dec = (meta >> 30) & 1u;
+        if (A <= kOneMaxAd)
+          one_stage_in(req, one_layout(A, L), ((A + 15u) >> 4) + ((L + 15u) >> 4) + dec, lds, lane, 64u);
+      }
+      if (lane < 4) {
+        cmd[4 * lane + 0] = c.x;
+        cmd[4 * lane + 1] = c.y;
+        cmd[4 * lane + 2] = c.z;
+        cmd[4 * lane + 3] = c.w;
+      }
+      if (lane == 0) cmd[0] = ex ? 0u : c.x;  // 0: leave
     }
     __syncthreads();
-    const uint64_t db = cmd[0], ex = cmd[1];
-    __syncthreads();  // cmd is rewritten only after every thread has read it
-    if (ex) break;
-    // the rest of the request line (nonce, key) was written before the
-    // doorbell: three 16-byte system-scope loads, all in flight together
-    u32x4 q[3];
-    {
-      const u32x4 *rq = reinterpret_cast<const u32x4 *>(reinterpret_cast<const uint8_t *>(ring) + 16);
-#if defined(__HIP_DEVICE_COMPILE__)
-      asm volatile("global_load_dwordx4 %0, %3, off sc0 sc1\n\t"
-                   "global_load_dwordx4 %1, %3, off offset:16 sc0 sc1\n\t"
-                   "global_load_dwordx4 %2, %3, off offset:32 sc0 sc1\n\t"
-                   "s_waitcnt vmcnt(0)"
-                   : "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]) : "v"(rq) : "memory");
-#else
-      for (int i = 0; i < 3; ++i) q[i] = rq[i];
-#endif
-    }
+    // chunk 0: seq, len | ad_len << 16 | decrypt << 30, nonce lo, hi;
+    // chunks 1..3: seq + key words 0..2, 3..5, 6..7
+    const uint32_t seq = cmd[0], meta = cmd[1];
     OneArgs a;
-    a.nonce = ((uint64_t)q[0].y << 32) | q[0].x;
-    a.key.w[0] = q[1].x; a.key.w[1] = q[1].y; a.key.w[2] = q[1].z; a.key.w[3] = q[1].w;
-    a.key.w[4] = q[2].x; a.key.w[5] = q[2].y; a.key.w[6] = q[2].z; a.key.w[7] = q[2].w;
+    a.nonce = ((uint64_t)cmd[3] << 32) | cmd[2];
+    a.key.w[0] = cmd[5]; a.key.w[1] = cmd[6]; a.key.w[2] = cmd[7];
+    a.key.w[3] = cmd[9]; a.key.w[4] = cmd[10]; a.key.w[5] = cmd[11];
+    a.key.w[6] = cmd[13]; a.key.w[7] = cmd[14];
+    __syncthreads();  // cmd is rewritten only after every thread has read it
+    if (seq == 0u) break;
     a.base = base;
-    a.len = (uint32_t)(db >> 32) & 0xffffu;
-    a.ad_len = (uint32_t)(db >> 48) & 0x3fffu;
-    const uint32_t dec = (uint32_t)(db >> 62) & 1u;
-    a.seq = (uint32_t)db;
-    if (a.ad_len > kOneMaxAd) a.ad_len = 0;  // the host never rings such a request
-    if (dec) one_body<true>(a, lds);
-    else one_body<false>(a, lds);
+    a.in_base = req;
+    a.len = meta & 0xffffu;
+    a.ad_len = (meta >> 16) & 0x3fffu;
+    a.seq = seq;
+    a.wipe_in = 1u;
+    a.staged = 1u;
+    const uint32_t dec = (meta >> 30) & 1u;
+    if (a.ad_len > kOneMaxAd) {  // the host never rings such a request
+      a.ad_len = 0;
+      a.staged = 0u;
+    }
+    // a speculation slot for exactly this (key, nonce)?
+    const uint32_t na = (a.ad_len + 15u) >> 4, nl = (a.len + 15u) >> 4;
+    const uint32_t nb = (a.len + 63u) >> 6;
+    int hit = -1;
+#pragma unroll
+    for (uint32_t i = 0; i < kSpecSlots; ++i) {
+      const SpecSlot &sp = slots[i];
+      bool m = sp.valid && sp.nlo == (uint32_t)a.nonce && sp.nhi == (uint32_t)(a.nonce >> 32) &&
+               nb <= sp.nks;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) m = m && sp.key[w] == a.key.w[w];
+      if (m) hit = (int)i;
+    }
+    const bool fast = hit >= 0 && na + nl + 1u <= kSpecPowers;
+    if (fast) {
+      if (dec) one_body_fast<true>(a, lds, &slots[hit], pre);
+      else one_body_fast<false>(a, lds, &slots[hit], pre);
+    } else {
+      if (dec) one_body<true>(a, lds);
+      else one_body<false>(a, lds);
+    }
+    last = seq;
+    // speculate on the next nonce under this key: the slot that holds the
+    // key, else the least recently used one; as many keystream blocks as this
+    // record used (at least 16, at most 63)
+    int dst = -1;
+#pragma unroll
+    for (uint32_t i = 0; i < kSpecSlots; ++i) {
+      bool m = slots[i].valid != 0u;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) m = m && slots[i].key[w] == a.key.w[w];
+      if (m) dst = (int)i;
+    }
+    if (dst < 0) dst = !slots[0].valid ? 0 : !slots[1].valid ? 1 : (slots[0].stamp <= slots[1].stamp ? 0 : 1);
+    nks = nb < 16u ? 16u : (nb > kSpecBlocks - 1u ? kSpecBlocks - 1u : nb);
+    __syncthreads();  // every thread chose the same slot before it changes
+    spec_fill(&slots[dst], pre, a.key.w, a.nonce + 1u, ++stamp, nks);
+#ifdef NOISE_ONE_TIMING
+    if (t == 0) reinterpret_cast<uint64_t *>(base)[8] = __builtin_amdgcn_s_memrealtime();
+#endif
 #pragma unroll
     for (int i = 0; i < 8; ++i) a.key.w[i] = 0u;
-    last = a.seq;
     t_last = __builtin_amdgcn_s_memrealtime();
   }
+  // leaving: no key or future keystream stays in this CU's LDS
+  {
+    uint32_t *w = reinterpret_cast<uint32_t *>(lds);
+    const size_t nw = (stage + kSpecSlots * sizeof(SpecSlot)) / 4 + kResCmdWords + kResPreWords;
+    for (size_t i = t; i < nw; i += kOneBlock) w[i] = 0u;
+  }
+  __syncthreads();
   // gone: the host's unload hook waits for this word (done line, offset 8)
-  if (threadIdx.x == 0) {
+  if (t == 0) {
     __threadfence_system();
     __hip_atomic_store(reinterpret_cast<uint32_t *>(base + 8), 0u, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
@@ -468,9 +849,9 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_resident(uint8_t *base, uint
 
 constexpr int kMaxAttrDev = 64;
 
-size_t one_lds_bytes(uint32_t ad_len, uint32_t len) {
-  const uint32_t na = (ad_len + 15u) >> 4, nl = (len + 15u) >> 4;
-  return 16ull * (na + nl + 4u + 8u);
+size_t resident_lds_bytes() {
+  return one_lds_bytes(kOneMaxAd, 65535u) + kSpecSlots * sizeof(SpecSlot) +
+         4u * (kResCmdWords + kResPreWords);
 }
 
 static hipError_t one_attr() {
@@ -491,19 +872,18 @@ static hipError_t one_attr() {
                               hipFuncAttributeMaxDynamicSharedMemorySize, max_lds);
     if (r == hipSuccess)
       r = hipFuncSetAttribute((const void *)k_aead_resident,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, max_lds);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)resident_lds_bytes());
     attr_err[dev] = r;
   });
   return attr_err[dev];
 }
 
-hipError_t launch_aead_resident(uint8_t *d_base, uint32_t last, uint32_t idle_us,
+hipError_t launch_aead_resident(uint8_t *d_req, uint8_t *d_base, uint32_t last, uint32_t idle_us,
                                 hipStream_t stream) {
   const hipError_t e = one_attr();
   if (e != hipSuccess) return e;
-  const size_t lds = one_lds_bytes(kOneMaxAd, 65535u);
-  hipLaunchKernelGGL(k_aead_resident, dim3(1), dim3(kOneBlock), lds, stream, d_base, last,
-                     (uint64_t)idle_us * 100ull);  // s_memrealtime: 100 MHz
+  hipLaunchKernelGGL(k_aead_resident, dim3(1), dim3(kOneBlock), resident_lds_bytes(), stream, d_req,
+                     d_base, last, (uint64_t)idle_us * 100ull);  // s_memrealtime: 100 MHz
   return hipGetLastError();
 }
 
@@ -516,9 +896,12 @@ hipError_t launch_aead_one(bool decrypt, const uint32_t key[8], uint64_t nonce,
   for (int i = 0; i < 8; ++i) a.key.w[i] = key[i];
   a.nonce = nonce;
   a.base = d_base;
+  a.in_base = d_base;
   a.len = len;
   a.ad_len = ad_len;
   a.seq = seq;
+  a.wipe_in = 0u;
+  a.staged = 0u;
   const size_t lds = one_lds_bytes(ad_len, len);
   if (decrypt)
     hipLaunchKernelGGL((k_aead_one<true>), dim3(1), dim3(kOneBlock), lds, stream, a);

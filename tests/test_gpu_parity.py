@@ -480,6 +480,51 @@ def test_resident_latency_path(oracle, golden):
     torch.cuda.synchronize()  # nothing left running on the device
 
 
+@pytest.mark.parametrize("req", ["fine", "host"])
+def test_resident_speculated_runs(oracle, req, monkeypatch):
+    """Resident mode speculates on (key, n + 1) after serving (key, n):
+    consecutive nonces under two interleaved keys (a session's send and
+    receive states) take the precomputed keystream + r-power path
+    (single_kernels.hip one_body_fast) from the second record of a run on.
+    Every size around its limits (63 keystream blocks, 256 Poly1305 blocks)
+    and past them, AD, tampering on the speculated path, a wrong nonce --
+    bit-exact vs the oracle, for each place the request image can live
+    (NOISE_GPU_RESIDENT_REQ)."""
+    monkeypatch.setenv("NOISE_GPU_RESIDENT_REQ", req)
+    noise_amd.set_resident(False)  # a fresh request image, of this kind
+    noise_amd.set_resident(True, 2000000)
+    try:
+        rng = random.Random(77)
+        keys = [rng.randbytes(32), rng.randbytes(32)]
+        for length in (0, 1, 16, 17, 1000, 1024, 3952, 4032, 4033, 4096, 16384, 65535):
+            for ad_len in (0, 64):
+                base = [rng.getrandbits(63), rng.getrandbits(63)]
+                for i in range(4):
+                    for w in (0, 1):
+                        n = base[w] + i
+                        ad, pt = rng.randbytes(ad_len), rng.randbytes(length)
+                        ct = noise_amd.encrypt_host(keys[w], n, ad, pt)
+                        assert ct == oracle.encrypt(keys[w], n, ad, pt), (length, ad_len, i, w)
+                # decrypt run under key 0: n misses, n + 1 .. hit; one tampered
+                for i in range(4):
+                    n = base[0] + 100 + i
+                    ad, pt = rng.randbytes(ad_len), rng.randbytes(length)
+                    ct = oracle.encrypt(keys[0], n, ad, pt)
+                    if i == 2:
+                        bad = bytearray(ct)
+                        bad[rng.randrange(len(bad))] ^= 4
+                        with pytest.raises(noise_amd.NoiseGpuError) as e:
+                            noise_amd.decrypt_host(keys[0], n, ad, bytes(bad))
+                        assert e.value.code == noise_amd.E_MAC
+                    else:
+                        assert noise_amd.decrypt_host(keys[0], n, ad, ct) == pt
+                # the speculated slot holds n + 1 of key 0: a record of another nonce
+                with pytest.raises(noise_amd.NoiseGpuError):
+                    noise_amd.decrypt_host(keys[0], base[0] + 104, ad, oracle.encrypt(keys[0], 7, ad, pt))
+    finally:
+        noise_amd.set_resident(False)
+
+
 def test_cipherstate_cpp_surface():
     """The drop-in noise::CipherState (C++20) on the golden records."""
     exe = os.path.join(noise_amd.ROOT, "noise-cpp_amd", "bin", "cipherstate_test")

@@ -19,6 +19,7 @@
 #include <mutex>
 #include <barrier>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <thread>
@@ -65,16 +66,28 @@ struct Wave {
   uint64_t xch[64];
 };
 
+// per emulated GPU thread: its ids, wave, the block's barrier
+// (__syncthreads) and dynamic LDS, the launch geometry -- thread-local, so an
+// asynchronous launch (below) runs beside synchronous ones
 struct Ctx {
   dim3 tid, bid;
   Wave *wave = nullptr;
   int lane = 0;
+  std::barrier<> *bar = nullptr;
+  unsigned char *dyn = nullptr;
+  dim3 grid, block;
 };
 inline thread_local Ctx ctx;
-inline dim3 grid_dim, block_dim;
-// the running block's barrier (__syncthreads) and dynamic LDS
-inline std::barrier<> *block_bar = nullptr;
-inline unsigned char *dyn_lds = nullptr;
+#define dyn_lds ctx.dyn  // kernels read emu::dyn_lds
+
+// Launches run synchronously, except one kernel a test names in
+// async_kernel (the resident latency kernel): it runs on a thread of its own
+// until it returns, like a kernel the host keeps polling, and the stream
+// queries / synchronisations below see it.
+inline void *async_kernel = nullptr;
+inline std::atomic<int> async_running{0};
+inline std::mutex async_mu;
+inline std::vector<std::thread> async_threads;
 
 // every hipMalloc / hipHostMalloc allocation, for tests that inspect what
 // the engine leaves in its buffers (secret hygiene)
@@ -135,17 +148,13 @@ inline uint64_t ballot(bool p) {
 
 // run kernel(args...) over the grid: blocks in sequence, threads in parallel
 template <class K, class... A>
-void launch_shm(K kernel, dim3 g, dim3 b, size_t shmem, A... args) {
-  grid_dim = g;
-  block_dim = b;
+void run_grid(K kernel, dim3 g, dim3 b, size_t shmem, A... args) {
   const unsigned nt = b.x;
   const unsigned nw = (nt + 63) / 64;
   for (unsigned bx = 0; bx < g.x; ++bx) {
     std::vector<Wave> waves(nw);
     std::barrier<> bar((std::ptrdiff_t)nt);
-    block_bar = &bar;
     std::vector<unsigned char> lds(shmem + 16, 0xCD);  // LDS is not zeroed on a GPU either
-    dyn_lds = lds.data();
     std::vector<std::thread> th;
     th.reserve(nt);
     for (unsigned t = 0; t < nt; ++t) {
@@ -154,13 +163,36 @@ void launch_shm(K kernel, dim3 g, dim3 b, size_t shmem, A... args) {
         ctx.bid = dim3(bx);
         ctx.wave = &waves[t / 64];
         ctx.lane = (int)(t % 64);
+        ctx.bar = &bar;
+        ctx.dyn = lds.data();
+        ctx.grid = g;
+        ctx.block = b;
         kernel(args...);
       });
     }
     for (auto &x : th) x.join();
-    block_bar = nullptr;
-    dyn_lds = nullptr;
   }
+}
+template <class K, class... A>
+void launch_shm(K kernel, dim3 g, dim3 b, size_t shmem, A... args) {
+  if (async_kernel && reinterpret_cast<void *>(kernel) == async_kernel) {
+    ++async_running;
+    std::lock_guard<std::mutex> lk(async_mu);
+    async_threads.emplace_back([=] {
+      run_grid(kernel, g, b, shmem, args...);
+      --async_running;
+    });
+    return;
+  }
+  run_grid(kernel, g, b, shmem, args...);
+}
+inline void async_join() {
+  std::vector<std::thread> th;
+  {
+    std::lock_guard<std::mutex> lk(async_mu);
+    th.swap(async_threads);
+  }
+  for (auto &x : th) x.join();
 }
 template <class K, class... A>
 void launch(K kernel, dim3 g, dim3 b, A... args) {
@@ -169,7 +201,7 @@ void launch(K kernel, dim3 g, dim3 b, A... args) {
 
 }  // namespace emu
 
-#define __syncthreads() (emu::block_bar->arrive_and_wait())
+#define __syncthreads() (emu::ctx.bar->arrive_and_wait())
 #define __threadfence_system() ((void)0)
 #define __ATOMIC_RELAXED_ __ATOMIC_RELAXED
 #define __HIP_MEMORY_SCOPE_SYSTEM 0
@@ -183,8 +215,8 @@ void launch(K kernel, dim3 g, dim3 b, A... args) {
 
 #define threadIdx (emu::ctx.tid)
 #define blockIdx (emu::ctx.bid)
-#define gridDim (emu::grid_dim)
-#define blockDim (emu::block_dim)
+#define gridDim (emu::ctx.grid)
+#define blockDim (emu::ctx.block)
 
 template <class T>
 inline T __shfl(T v, int src, int width = 64) {
@@ -219,6 +251,19 @@ inline uint64_t __ballot(int p) { return emu::ballot(p != 0); }
 #define __builtin_amdgcn_mov_dpp(v, ctrl, rm, bm, bc)                            \
   ((int)emu::shfl((uint32_t)(v), (emu::ctx.lane & ~3) |                          \
                                      (((ctrl) >> (2 * (emu::ctx.lane & 3))) & 3)))
+// update_dpp with old = 0 and all rows / banks enabled, for the controls the
+// kernels use: quad_perm (< 0x100) and row_ror:n (0x121..0x12f)
+#define __builtin_amdgcn_update_dpp(old, v, ctrl, rm, bm, bc) emu::dpp_ror((v), (ctrl))
+namespace emu {
+inline int dpp_ror(int v, int ctrl) {
+  const int lane = ctx.lane;
+  int src;
+  if (ctrl < 0x100) src = (lane & ~3) | ((ctrl >> (2 * (lane & 3))) & 3);
+  else if (ctrl >= 0x121 && ctrl <= 0x12f) src = (lane & ~15) | ((lane + (ctrl - 0x120)) & 15);
+  else std::abort();
+  return (int)shfl((uint32_t)v, src);
+}
+}  // namespace emu
 #define __builtin_amdgcn_fence(...) ((void)0)
 // lanes of a real wave run in lockstep; here they meet at every wave_barrier
 // (the kernels put one after each LDS hand-off between lanes)
@@ -261,6 +306,11 @@ inline hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
 inline hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned) { return hipSuccess; }
 inline hipError_t hipGetDevice(int *d) { *d = 0; return hipSuccess; }
 inline hipError_t hipMalloc(void **p, size_t n) {
+  *p = emu::track(std::calloc(n ? n : 1, 1), n, false);
+  return *p ? hipSuccess : hipErrorMemoryAllocation;
+}
+#define hipDeviceMallocFinegrained 1u
+inline hipError_t hipExtMallocWithFlags(void **p, size_t n, unsigned) {
   *p = emu::track(std::calloc(n ? n : 1, 1), n, false);
   return *p ? hipSuccess : hipErrorMemoryAllocation;
 }
@@ -314,8 +364,13 @@ inline hipError_t hipMemsetAsync(void *p, int v, size_t n, hipStream_t) {
 }
 
 enum { hipErrorNotReady = 600 };
-inline hipError_t hipStreamQuery(hipStream_t) { return hipSuccess; }
-inline hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+inline hipError_t hipStreamQuery(hipStream_t) {
+  return emu::async_running.load() ? (hipError_t)hipErrorNotReady : hipSuccess;
+}
+inline hipError_t hipStreamSynchronize(hipStream_t) {
+  emu::async_join();
+  return hipSuccess;
+}
 inline hipError_t hipStreamDestroy(hipStream_t) { return hipSuccess; }
 inline hipError_t hipEventDestroy(hipEvent_t) { return hipSuccess; }
 inline hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }

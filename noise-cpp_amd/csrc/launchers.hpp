@@ -59,13 +59,31 @@ struct OneRing {
 };
 static_assert(sizeof(OneRing) == 64, "stop line");
 // Resident request image (OneReq; device memory the host writes through the
-// BAR, or host-mapped): [0,64) the request line -- four 16-byte chunks, each
-// {seq, w1, w2, w3}:
+// BAR, or host-mapped): kReqChunks 16-byte chunks, each {seq, w1, w2, w3},
+// that the kernel polls:
 //   chunk 0: seq, len | ad_len << 16 | decrypt << 30, nonce lo, nonce hi
 //   chunk 1: seq, key words 0, 1, 2      chunk 2: seq, key words 3, 4, 5
 //   chunk 3: seq, key words 6, 7, 0
-// then AD | record | tag at one_layout() offsets (output goes to the host
-// image).  The kernel zeroes all but the seq words after each request.
+//   chunks 4 ..: a small record INLINE -- its staged image (AD | pad |
+//     record | pad | tag, the 16-byte pieces the kernel works on) 12 bytes
+//     per chunk, so every chunk carries the seq that validates it and the
+//     record arrives with the poll that finds the request (req_inline)
+// then, at kReqStageOff, a larger record's AD | record | tag at one_layout()
+// offsets, loaded by DMA once the request is seen.  Output goes to the host
+// image.  The kernel zeroes the request after use (but for the header
+// chunks' seq words).
+constexpr uint32_t kReqChunks = 128;
+constexpr uint32_t kReqInlineBytes = 12u * (kReqChunks - 4u);  // 1488
+constexpr uint64_t kReqStageOff = 16ull * kReqChunks;
+__host__ __device__ constexpr uint32_t req_image_bytes(uint32_t ad_len, uint32_t len, bool decrypt) {
+  return 16u * (((ad_len + 15u) >> 4) + ((len + 15u) >> 4) + (decrypt ? 1u : 0u));
+}
+__host__ __device__ constexpr bool req_inline(uint32_t ad_len, uint32_t len, bool decrypt) {
+  return req_image_bytes(ad_len, len, decrypt) <= kReqInlineBytes;
+}
+__host__ __device__ constexpr uint32_t req_inline_chunks(uint32_t ad_len, uint32_t len, bool decrypt) {
+  return req_inline(ad_len, len, decrypt) ? (req_image_bytes(ad_len, len, decrypt) + 11u) / 12u : 0u;
+}
 __host__ __device__ constexpr OneLayout one_layout(uint32_t ad_len, uint32_t len) {
   const uint64_t a16 = (ad_len + 15ull) & ~15ull, l16 = (len + 15ull) & ~15ull;
   OneLayout o{};
@@ -76,7 +94,9 @@ __host__ __device__ constexpr OneLayout one_layout(uint32_t ad_len, uint32_t len
   o.total = o.out + l16 + 16;
   return o;
 }
-constexpr uint64_t kOneReqBytes = one_layout(kOneMaxAd, 65535u).total;
+constexpr uint64_t kOneReqBytes = kReqStageOff + one_layout(kOneMaxAd, 65535u).total;
+// the resident kernel's records: <= 63 keystream blocks (its quad path)
+constexpr uint32_t kResidentMaxLen = 63u * 64u;
 // dynamic LDS of the latency kernels: staged pieces + tag, r, s, verdict and
 // the per-wave Poly1305 sums
 __host__ __device__ constexpr size_t one_lds_bytes(uint32_t ad_len, uint32_t len) {

@@ -37,13 +37,17 @@ int hip_fail(hipError_t e, const char *what) {
 
 // Is a gfx950 device current?  Cached per thread and device.
 int check_device() {
+  // per thread: the device last checked and its verdict -- the single-record
+  // path calls this per record, so a known device costs one hipGetDevice
   thread_local int cached_dev = -1, cached_ok = 0;
+  int dev = 0;
+  if (cached_dev >= 0 && hipGetDevice(&dev) == hipSuccess && dev == cached_dev)
+    return cached_ok ? NOISE_GPU_OK : NOISE_GPU_E_NODEV;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
     g_last_error = "no HIP device visible";
     return NOISE_GPU_E_NODEV;
   }
-  int dev = 0;
   HIP_TRY(hipGetDevice(&dev));
   if (dev == cached_dev) return cached_ok ? NOISE_GPU_OK : NOISE_GPU_E_NODEV;
   hipDeviceProp_t prop;
@@ -221,6 +225,10 @@ struct OneCtx {
   // resident request image (OneReq, launchers.hpp): host and device views
   uint8_t *hreq = nullptr, *dreq = nullptr;
   int req_kind = kReqFine;
+  // the launch path's stream while in resident mode (the resident instance
+  // occupies `stream`): records the resident kernel does not serve
+  hipStream_t lstream_res = nullptr;
+  hipStream_t lstream = nullptr;
   ~OneCtx() { release(); }
   noise_amd::OneRing *ring() { return reinterpret_cast<noise_amd::OneRing *>(h + noise_amd::kOneRingOff); }
   // stop word -> the instance leaves at its next poll; wait for it
@@ -268,6 +276,11 @@ struct OneCtx {
     stop_resident();
     if (stream) (void)hipStreamSynchronize(stream);
     release_req();
+    if (lstream_res) {
+      (void)hipStreamSynchronize(lstream_res);
+      (void)hipStreamDestroy(lstream_res);
+      lstream_res = nullptr;
+    }
     if (h) {
       std::memset(h, 0, cap);
       (void)hipHostFree(h);
@@ -319,21 +332,24 @@ struct OneCtx {
   // A record takes microseconds; no answer within kOneWaitLimit means the
   // kernel cannot see the request (or is wedged): stop it and fail the call
   // rather than spin for ever.
-  int wait(uint32_t s) {
+  // by_resident: the request went to the resident instance (else a launch on
+  // lstream, the launch path's stream)
+  int wait(uint32_t s, bool by_resident) {
+    hipStream_t wst = by_resident ? stream : lstream;
     volatile uint32_t *done = reinterpret_cast<volatile uint32_t *>(h);
     const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t spin = 0;; ++spin) {
       if (*done == s) return NOISE_GPU_OK;
       if ((spin & 1023u) == 1023u) {  // now and then: has the stream failed or ended?
         if (std::chrono::steady_clock::now() - t0 > kOneWaitLimit) {
-          if (resident) stop_resident();
+          if (by_resident) stop_resident();
           g_last_error = "latency kernel gave no answer within 10 s";
           return NOISE_GPU_E_HIP;
         }
-        const hipError_t e = hipStreamQuery(stream);
+        const hipError_t e = hipStreamQuery(wst);
         if (e == hipSuccess) {
           if (*done == s) return NOISE_GPU_OK;
-          if (resident && launched) {  // the instance idled out before the doorbell
+          if (by_resident && launched) {  // the instance idled out before the doorbell
             const int rc = launch_resident(s - 1u);
             if (rc) return rc;
             continue;
@@ -393,19 +409,48 @@ int one_record(bool dec, const uint8_t key[32], uint64_t nonce, const uint8_t *a
                                 : lay.total);
   if (rc) return rc;
   if (c.resident && (rc = c.reserve_req())) return rc;
-  uint8_t *img = c.resident ? c.hreq : c.h;  // where the input is staged
-  if (ad_len) std::memcpy(img + lay.ad, ad, ad_len);
-  if (len) std::memcpy(img + lay.in, in, len);
-  if (dec) std::memcpy(img + lay.tag, tag, 16);
+  // the resident kernel serves records of <= 63 keystream blocks; a bigger
+  // one is a launch (a second stream: the resident instance holds the first)
+  const bool res = c.resident && len <= noise_amd::kResidentMaxLen;
+  c.lstream = c.stream;
+  if (c.resident && !res) {
+    if (!c.lstream_res) HIP_TRY(hipStreamCreateWithFlags(&c.lstream_res, hipStreamNonBlocking));
+    c.lstream = c.lstream_res;
+  }
   uint32_t s = ++c.seq;
   if (s == 0) s = c.seq = 1;
+  const uint32_t n_inl = res ? noise_amd::req_inline_chunks(ad_len, len, dec) : 0u;
+  if (n_inl) {
+    // a small record goes inline: its staged image (AD | pad | record | pad
+    // | tag) 12 bytes per 16-byte chunk {seq, 3 words} (launchers.hpp OneReq)
+    alignas(16) uint8_t im[noise_amd::kReqInlineBytes + 12];
+    const uint32_t na16 = (ad_len + 15u) & ~15u, nl16 = (len + 15u) & ~15u;
+    std::memset(im, 0, 12u * n_inl);
+    if (ad_len) std::memcpy(im, ad, ad_len);
+    if (len) std::memcpy(im + na16, in, len);
+    if (dec) std::memcpy(im + na16 + nl16, tag, 16);
+    __m128i *q = reinterpret_cast<__m128i *>(c.hreq) + 4;
+    for (uint32_t i = 0; i < n_inl; ++i) {
+      uint32_t w[3];
+      std::memcpy(w, im + 12u * i, 12);
+      _mm_store_si128(q + i, _mm_setr_epi32((int)s, (int)w[0], (int)w[1], (int)w[2]));
+    }
+    explicit_bzero(im, 12u * n_inl);  // the plaintext copy on the stack goes too
+  } else {
+    // staged in place: the launch path's host image, or the resident
+    // request image's DMA area
+    uint8_t *img = res ? c.hreq + noise_amd::kReqStageOff : c.h;
+    if (ad_len) std::memcpy(img + lay.ad, ad, ad_len);
+    if (len) std::memcpy(img + lay.in, in, len);
+    if (dec) std::memcpy(img + lay.tag, tag, 16);
+  }
   uint32_t k[8];
   key_words(key, k);
-  if (c.resident) {
+  if (res) {
     // the request line: four 16-byte chunks, each {seq, 3 payload words},
     // stored whole (16-byte aligned SSE stores) after an sfence that orders
     // them behind the staged bytes (write-combined device memory); the GPU
-    // takes the request once all four carry seq (launchers.hpp OneReq)
+    // takes the request once all four (and any inline chunks) carry seq
     _mm_sfence();
     const uint32_t meta = len | (ad_len << 16) | ((uint32_t)dec << 30);
     __m128i *q = reinterpret_cast<__m128i *>(c.hreq);
@@ -417,11 +462,11 @@ int one_record(bool dec, const uint8_t key[32], uint64_t nonce, const uint8_t *a
     _mm_sfence();
     if (!c.launched) rc = c.launch_resident(s - 1u);
   } else {
-    const hipError_t e = noise_amd::launch_aead_one(dec, k, nonce, c.d, len, ad_len, s, c.stream);
+    const hipError_t e = noise_amd::launch_aead_one(dec, k, nonce, c.d, len, ad_len, s, c.lstream);
     if (e != hipSuccess) rc = hip_fail(e, "launch_aead_one");
   }
   std::memset(k, 0, sizeof k);
-  if (rc == NOISE_GPU_OK) rc = c.wait(s);
+  if (rc == NOISE_GPU_OK) rc = c.wait(s, res);
   if (rc == NOISE_GPU_OK) {
     std::atomic_thread_fence(std::memory_order_acquire);
     const uint32_t status = dec ? reinterpret_cast<volatile uint32_t *>(c.h)[1] : 0u;
@@ -436,7 +481,7 @@ int one_record(bool dec, const uint8_t key[32], uint64_t nonce, const uint8_t *a
   // hygiene: status, AD, record, output (the resident kernel zeroes its
   // request image itself before the done word; an error path does it here)
   std::memset(c.h + 4, 0, 4);
-  if (c.resident) {
+  if (res) {
     std::memset(c.h + lay.out, 0, lay.total - lay.out);
     if (rc != NOISE_GPU_OK && c.hreq) {
       c.stop_resident();

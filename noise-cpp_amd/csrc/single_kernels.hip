@@ -51,8 +51,11 @@ struct OneArgs {
   uint32_t len, ad_len;
   uint32_t seq;         // written to the done word last
   uint32_t wipe_in;     // zero the staged input (request image) before the done word
-  uint32_t staged;      // the input is already on its way into LDS (the resident
-                        // kernel's polling wave issued the DMA): only wait for it
+  uint32_t staged;      // the input is already in (or on its way into) LDS: the
+                        // resident kernel's polling wave unpacked or issued it
+  uint8_t *req;         // resident: the request image (header / inline chunks)
+  uint32_t n_inl;       // resident: inline chunks of this request (zeroed after use)
+  uint32_t dec;         // RT bodies: the direction (the resident kernel's one copy)
 };
 
 // The staged input pieces [0, npc) -> LDS[0, npc) by LDS-DMA (AD pieces, then
@@ -85,6 +88,17 @@ __device__ __forceinline__ void st_sys16(uint8_t *base, uint64_t off, u32x4 w) {
 #endif
 }
 
+// The resident kernel's request image after use: the header chunks keep
+// only their seq word, the inline chunks are zeroed (threads u of nthr)
+__device__ __forceinline__ void req_wipe(const OneArgs &a, uint32_t u, uint32_t nthr) {
+  if (u < 4) {
+    const u32x4 w = {a.seq, 0u, 0u, 0u};
+    st_sys16(a.req, 16ull * u, w);
+  }
+  const u32x4 z = {0u, 0u, 0u, 0u};
+  for (uint32_t k = u; k < a.n_inl; k += nthr) st_sys16(a.req, 16ull * (4u + k), z);
+}
+
 // x * y by binary exponentiation: x^e (e >= 1)
 __device__ __forceinline__ F26 pow26(F26 x, uint32_t e) {
   F26 r = x;
@@ -103,14 +117,26 @@ __device__ __forceinline__ F26 add26(const F26 &a, const F26 &b) {
   return r;
 }
 
-// tools/ubench/one_timing.hip builds this file with NOISE_ONE_TIMING: thread
-// 0 stamps s_memrealtime at the phase boundaries into the done line
+// tools/ubench/one_timing.hip and resident_timing.hip build this file with
+// NOISE_ONE_TIMING: s_memrealtime stamps at the phase boundaries go to LDS
+// (a store to the host image would put a PCIe write into the next vmcnt
+// wait) and are copied to the last 64 bytes of the host image afterwards
+// (kOneTsOff): by one_finish before the done word (launch path), after the
+// speculation (resident).
 #ifdef NOISE_ONE_TIMING
-#define NOISE_ONE_STAMP(i)                                                       \
+__shared__ uint64_t g_one_ts[8];
+#define NOISE_ONE_STAMP(i) \
+  if (threadIdx.x == 0) g_one_ts[i] = __builtin_amdgcn_s_memrealtime()
+#define NOISE_FAST_STAMP(i) \
+  if (threadIdx.x == 64) g_one_ts[i] = __builtin_amdgcn_s_memrealtime()
+constexpr uint64_t kOneTsOff = one_layout(kOneMaxAd, 65535u).total - 64u;
+#define NOISE_TS_FLUSH(b)                                                        \
   if (threadIdx.x == 0)                                                          \
-    reinterpret_cast<uint64_t *>(a.base)[2 + (i)] = __builtin_amdgcn_s_memrealtime()
+    for (int i_ = 0; i_ < 8; ++i_) reinterpret_cast<uint64_t *>((b) + kOneTsOff)[i_] = g_one_ts[i_]
 #else
 #define NOISE_ONE_STAMP(i) ((void)0)
+#define NOISE_FAST_STAMP(i) ((void)0)
+#define NOISE_TS_FLUSH(b) ((void)0)
 #endif
 
 // Step 5 of every single-record body: the resident kernel's request image
@@ -126,11 +152,9 @@ __device__ __forceinline__ void one_finish(const OneArgs &a, const OneLayout &la
   const uint32_t t = threadIdx.x;
   if (a.wipe_in) {
     const u32x4 z = {0u, 0u, 0u, 0u};
-    for (uint32_t i = t; i < npc; i += kOneBlock) st_sys16(a.in_base, lay.ad + 16ull * i, z);
-    if (t < 4) {
-      const u32x4 w = {a.seq, 0u, 0u, 0u};
-      st_sys16(a.in_base, 16ull * t, w);
-    }
+    if (!a.n_inl)
+      for (uint32_t i = t; i < npc; i += kOneBlock) st_sys16(a.in_base, lay.ad + 16ull * i, z);
+    req_wipe(a, t, kOneBlock);
   }
 #ifdef NOISE_ONE_SYSFENCE  // A/B (tools/ubench/one_timing): the full system release
   __threadfence_system();
@@ -140,6 +164,7 @@ __device__ __forceinline__ void one_finish(const OneArgs &a, const OneLayout &la
 #endif
   __syncthreads();
   NOISE_ONE_STAMP(5);
+  if (!a.wipe_in) NOISE_TS_FLUSH(a.base);  // launch path (one_timing)
   if (t == 0)
     __hip_atomic_store(reinterpret_cast<uint32_t *>(a.base), a.seq, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
@@ -148,8 +173,13 @@ __device__ __forceinline__ void one_finish(const OneArgs &a, const OneLayout &la
 // One record, the whole workgroup (k_aead_one: one launch per record;
 // k_aead_resident: a resident workgroup serving a doorbell ring).
 
-template <bool DECRYPT>
+// RT (the resident kernel): ONE copy for both directions (a.dec at run time)
+// and only the quad keystream path -- the kernel serves records of <= 63
+// keystream blocks (bigger ones take the launch path) and must stay small:
+// its poll loop, bodies and speculation share one instruction cache.
+template <bool DECRYPT_T, bool RT = false>
 __device__ __forceinline__ void one_body(const OneArgs &a, uint4 *lds) {
+  const bool DECRYPT = RT ? a.dec != 0u : DECRYPT_T;
   NOISE_ONE_STAMP(0);
   const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
   const uint32_t L = a.len, A = a.ad_len;
@@ -171,7 +201,7 @@ __device__ __forceinline__ void one_body(const OneArgs &a, uint4 *lds) {
   // ones: block b on thread b % 256.
   const uint32_t nlo = (uint32_t)a.nonce, nhi = (uint32_t)(a.nonce >> 32);
   const uint32_t nb = (L + 63u) >> 6;
-  const bool quad = nb < 64u;  // workgroup-uniform
+  const bool quad = RT || nb < 64u;  // workgroup-uniform
   uint32_t ks[kOneMaxKsPerThread][16];
   uint32_t kq[4] = {0u, 0u, 0u, 0u};
   uint32_t *lds32 = reinterpret_cast<uint32_t *>(lds);
@@ -442,43 +472,68 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_one(const OneArgs a) {
 //     speculation slots (future keystream, key copies) are zeroed in LDS.
 // `last` is the seq already served when this instance started: a request
 // rung while an idle instance was exiting is picked up by the next one.
-constexpr uint32_t kSpecBlocks = 64;   // keystream blocks 0..63 of the next nonce
+constexpr uint32_t kSpecBlocks = 64;   // keystream blocks 1..63 of the next nonce
 constexpr uint32_t kSpecPowers = 256;  // r^1 .. r^256
-constexpr uint32_t kSpecSlots = 2;
-struct SpecSlot {                      // LDS, 9328 B
-  uint32_t key[8];
-  uint32_t nlo, nhi, valid, stamp;     // stamp: last use (LRU)
-  uint32_t r[4], s[4];
-  uint32_t nks;                        // keystream blocks 1..nks are speculated
-  uint32_t pad[7];
+constexpr uint32_t kSpecSlots = 2;     // speculated (key, nonce)s: a session's two directions
+constexpr uint32_t kSpecBufs = 3;      // tables: one per slot + the one being filled
+constexpr uint32_t kFastMaxBlocks = 192;  // Poly1305 blocks of the fast path (waves 1..3)
+struct SpecBuf {                       // LDS, 9216 B
   uint32_t ks[kSpecBlocks * 16];       // block b word w at ks[16 b + w] (b >= 1)
   uint32_t pw[kSpecPowers * 5];        // r^e (radix 2^26) at pw[5 (e - 1)]
 };
-static_assert(sizeof(SpecSlot) % 16 == 0, "slot alignment");
-// LDS words after the slots: the request broadcast (16), the next nonce's
-// block-0 words r0..3 (clamped), s0..3 and a valid flag (9)
-constexpr uint32_t kResCmdWords = 16, kResPreWords = 16;
+struct SpecSlot {                      // LDS, 96 B
+  uint32_t key[8];
+  uint32_t nlo, nhi, valid, stamp;     // stamp: last use (LRU)
+  uint32_t r[4], s[4];
+  uint32_t nks, pmax, buf, pad;        // keystream blocks 1..nks, powers r^1..r^pmax, in bufs[buf]
+};
+// LDS words after the slots: the request broadcast (16 + the inline chunk
+// count); the next nonce's
+// block-0 words r0..3 (clamped), s0..3 and a valid flag; the fast path's
+// wave-group counter and the spare table's index
+constexpr uint32_t kResCmdWords = 20, kResPreWords = 16, kResSyncWords = 16;
+__host__ __device__ constexpr size_t resident_lds_bytes() {
+  return one_lds_bytes(kOneMaxAd, 65535u) + kSpecBufs * sizeof(SpecBuf) +
+         kSpecSlots * sizeof(SpecSlot) + 4u * (kResCmdWords + kResPreWords + kResSyncWords);
+}
 
-__device__ __forceinline__ F26 pw_get(const SpecSlot *sp, uint32_t e) {
+__device__ __forceinline__ F26 pw_get(const SpecBuf *b, uint32_t e) {
   F26 f;
 #pragma unroll
-  for (int i = 0; i < 5; ++i) f.a[i] = sp->pw[5u * (e - 1u) + i];
+  for (int i = 0; i < 5; ++i) f.a[i] = b->pw[5u * (e - 1u) + i];
   return f;
 }
-__device__ __forceinline__ void pw_put(SpecSlot *sp, uint32_t e, const F26 &f) {
+__device__ __forceinline__ void pw_put(SpecBuf *b, uint32_t e, const F26 &f) {
 #pragma unroll
-  for (int i = 0; i < 5; ++i) sp->pw[5u * (e - 1u) + i] = f.a[i];
+  for (int i = 0; i < 5; ++i) b->pw[5u * (e - 1u) + i] = f.a[i];
 }
 // program-order LDS hand-off within ONE wave (no workgroup barrier)
 __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
 }
+// LDS counter hand-offs between the waves of a group that do not all reach
+// a workgroup barrier (the fast path: wave 0 speculates while waves 1..3
+// serve the record): lane 0 of a wave arrives, any wave waits for a count
+__device__ __forceinline__ void grp_arrive(uint32_t *c, uint32_t lane) {
+  wave_sync_lds();  // every lane of the wave is here (lockstep on a GPU; the emulator's lanes are threads)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (lane == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// one thread's arrival (from code only that thread runs)
+__device__ __forceinline__ void grp_arrive1(uint32_t *c) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void grp_wait(uint32_t *c, uint32_t n) {
+  while (__hip_atomic_load(c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < n)
+    __builtin_amdgcn_s_sleep(1);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
 
 // Block 0 of (key, nonce) on the quad of threads 0..3: pre[q] = r word q
 // (clamped), pre[4 + q] = s word q, pre[8] = 1.  Called by all of wave 0
-// (every quad computes, the first one stores: no divergence around the DPP)
-// while the rest of the workgroup waits for its data.
+// (every quad computes, the first one stores: no divergence around the DPP).
 __device__ __forceinline__ void spec_block0(uint32_t *pre, const uint32_t key[8], uint64_t nonce,
                                             uint32_t lane) {
   uint32_t kq[4];
@@ -491,80 +546,78 @@ __device__ __forceinline__ void spec_block0(uint32_t *pre, const uint32_t key[8]
   }
 }
 
-// Fill slot sp for (key, nonce) with keystream blocks 1..nks (nks <= 63):
-// the whole workgroup.  pre: block 0 of (key, nonce) if pre[8] is set
-// (spec_block0 ran during the request), else it is computed here first.
-//   wave 0        : the power ladder r^1..r^16 and r^32..r^256 by 16s, in
-//                   LDS with wave-level ordering only (8 levels of one
-//                   product; no workgroup barrier between them);
-//   waves 1..3    : the keystream blocks, one per quad (48 at a time);
-//   all           : r^(16a + b) = r^(16a) r^b for the rest, one product each.
-__device__ void spec_fill(SpecSlot *sp, uint32_t *pre, const uint32_t key[8], uint64_t nonce,
-                          uint32_t stamp, uint32_t nks) {
-  const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
-  const uint32_t nlo = (uint32_t)nonce, nhi = (uint32_t)(nonce >> 32);
-  if (!pre[8]) {  // workgroup-uniform
-    if (wave == 0) spec_block0(pre, key, nonce, lane);
-    __syncthreads();
-  }
-  if (t == 0) sp->valid = 0u;
-  if (wave == 0) {
-    if (lane == 0) pw_put(sp, 1u, to26(pre[0], pre[1], pre[2], pre[3], 0u));
+// Wave 0: the power ladder into b from r = pre[0..3] -- r^1..r^16, then
+// r^32, r^48, .. by 16s up to 16 ceil(pmax / 16): one product per level,
+// LDS ordered within the wave only (no workgroup barrier between levels).
+__device__ void spec_ladder(SpecBuf *b, const uint32_t *pre, uint32_t pmax, uint32_t lane) {
+  if (lane == 0) pw_put(b, 1u, to26(pre[0], pre[1], pre[2], pre[3], 0u));
+  wave_sync_lds();
+  // r^(l + i) = r^l r^i, i = 1 .. l: r^1 .. r^16
+#pragma unroll 1
+  for (uint32_t l = 1; l <= 8; l <<= 1) {
+    if (lane < l) pw_put(b, l + lane + 1u, mul26(pw_get(b, l), pw_get(b, lane + 1u)));
     wave_sync_lds();
-    // r^(2^l + i) = r^(2^l) r^i, i = 1 .. 2^l: r^1 .. r^16
+  }
+  // r^(16 (l + i)) = r^(16 l) r^(16 i)
+  const uint32_t m16 = (pmax + 15u) >> 4;
 #pragma unroll 1
-    for (uint32_t l = 1; l <= 8; l <<= 1) {
-      if (lane < l) pw_put(sp, l + lane + 1u, mul26(pw_get(sp, l), pw_get(sp, lane + 1u)));
-      wave_sync_lds();
-    }
-    // r^(16 (2^l + i)) = r^(16 2^l) r^(16 i): the multiples of 16 up to 256
+  for (uint32_t l = 1; l < m16; l <<= 1) {
+    if (lane < l && l + lane + 1u <= m16)
+      pw_put(b, 16u * (l + lane + 1u), mul26(pw_get(b, 16u * l), pw_get(b, 16u * (lane + 1u))));
+    wave_sync_lds();
+  }
+}
+// Waves 1..3: keystream blocks 1..nks of (key, nonce) into b, one per quad.
+__device__ void spec_keystream(SpecBuf *b, const uint32_t key[8], uint64_t nonce, uint32_t nks,
+                               uint32_t t) {
+  const uint32_t wave = t >> 6, qd = (t - 64u) >> 2, wq0 = 16u * (wave - 1u);  // 48 quads
 #pragma unroll 1
-    for (uint32_t l = 1; l <= 8; l <<= 1) {
-      if (lane < l)
-        pw_put(sp, 16u * (l + lane + 1u), mul26(pw_get(sp, 16u * l), pw_get(sp, 16u * (lane + 1u))));
-      wave_sync_lds();
-    }
-  } else {
-    const uint32_t qd = (t - 64u) >> 2, wq0 = 16u * (wave - 1u);  // 48 quads; the wave's first
-#pragma unroll 1
-    for (uint32_t b0 = 1u + wq0; b0 <= nks; b0 += 48u) {  // wave-uniform trip count
-      const uint32_t b = b0 + (qd - wq0);
-      uint32_t kq[4];
-      chacha20_quad(key, t & 3u, b, nlo, nhi, kq);
-      if (b <= nks) {
+  for (uint32_t b0 = 1u + wq0; b0 <= nks; b0 += 48u) {  // wave-uniform trip count
+    const uint32_t blk = b0 + (qd - wq0);
+    uint32_t kq[4];
+    chacha20_quad(key, t & 3u, blk, (uint32_t)nonce, (uint32_t)(nonce >> 32), kq);
+    if (blk <= nks) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) sp->ks[16u * b + 4u * r + (t & 3u)] = kq[r];
-      }
+      for (int r = 0; r < 4; ++r) b->ks[16u * blk + 4u * r + (t & 3u)] = kq[r];
     }
   }
-  __syncthreads();
-  {  // the rest: r^(16 a + b) = r^(16 a) r^b, a = 1..15, b = 1..15
+}
+// All threads: the powers that are not on the ladder, r^(16 a + c) = r^(16 a)
+// r^c (one product each), then slot dst takes (key, nonce) with table b.
+__device__ void spec_finish(SpecSlot *dst, uint32_t bi, SpecBuf *b, uint32_t *pre, uint32_t *sync,
+                            const uint32_t key[8], uint64_t nonce, uint32_t stamp, uint32_t nks,
+                            uint32_t pmax) {
+  const uint32_t t = threadIdx.x;
+  {
     const uint32_t e = t + 1u, hi = e >> 4, lo = e & 15u;
-    if (hi >= 1u && hi <= 15u && lo != 0u) pw_put(sp, e, mul26(pw_get(sp, 16u * hi), pw_get(sp, lo)));
-  }
-  if (t < 8) sp->key[t] = key[t];
-  if (t < 4) {
-    sp->r[t] = pre[t];
-    sp->s[t] = pre[4 + t];
+    if (e <= pmax && hi >= 1u && lo != 0u) pw_put(b, e, mul26(pw_get(b, 16u * hi), pw_get(b, lo)));
   }
   if (t == 0) {
-    sp->nlo = nlo;
-    sp->nhi = nhi;
-    sp->stamp = stamp;
-    sp->nks = nks;
+    sync[1] = dst->buf;  // the slot's old table is the next spare
+    dst->buf = bi;
+    dst->nlo = (uint32_t)nonce;
+    dst->nhi = (uint32_t)(nonce >> 32);
+    dst->stamp = stamp;
+    dst->nks = nks;
+    dst->pmax = pmax;
+  }
+  if (t < 8) dst->key[t] = key[t];
+  if (t < 4) {
+    dst->r[t] = pre[t];
+    dst->s[t] = pre[4 + t];
   }
   __syncthreads();
   if (t == 0) {
-    sp->valid = 1u;
+    dst->valid = 1u;
     pre[8] = 0u;
+    sync[0] = 0u;  // the group counter, for the next request
   }
   __syncthreads();
 }
 
-// Sum of v over the wave (every lane holds it): two quad_perm DPP adds and
-// two row_ror DPP adds give each lane its row's sum; the four row sums come
-// out through readlane (no LDS crossbar round trips).  The caller keeps the
-// row sums below 2^32.
+// Sum of v over each row of 16 lanes (every lane of the row holds it): two
+// quad_perm and two row_ror DPP adds, no LDS crossbar round trips.  The
+// caller keeps the row sums below 2^32.
 __device__ __forceinline__ uint32_t row_sum_dpp(uint32_t v) {
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
@@ -577,18 +630,26 @@ __device__ __forceinline__ uint32_t rows_total(uint32_t v) {
          (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
 }
 
-// A speculated record: sp holds (key, nonce)'s keystream blocks 1..nks and
-// r^1..r^256; the record has <= nks keystream blocks and P = na + nl + 1 <=
-// 256 Poly1305 blocks.  Thread t < P takes block t (AD pieces, then
-// ciphertext pieces -- encrypt makes them here -- then the length block) and
-// computes (m_t + 2^128) r^(P-t); the 256 products are summed per wave by
-// DPP (radix 2^26 limbs, renormalised after 16 terms) and the four wave sums
-// by thread 0, which adds s and writes / checks the tag.  Same result as the
-// Horner chain of crypto_aead_write / crypto_aead_read (monocypher.c:2858-
-// 2929): the sum IS that polynomial evaluated at r.  While the record's data
-// is in flight, threads 0..3 compute block 0 of the next nonce (pre).
-template <bool DECRYPT>
-__device__ void one_body_fast(const OneArgs &a, uint4 *lds, const SpecSlot *sp, uint32_t *pre) {
+// A speculated record (sp: (key, nonce)'s keystream blocks 1..nks and
+// r^1..r^pmax in bufs[sp->buf]; the record has <= nks keystream blocks and
+// P = na + nl + 1 <= min(pmax, 192) Poly1305 blocks).
+//   waves 1..3: thread u = t - 64 < P takes block u (AD pieces, then
+//     ciphertext pieces -- encrypt makes them here -- then the length
+//     block) and computes (m_u + 2^128) r^(P-u); the products are summed per
+//     wave by DPP (radix 2^26 limbs, renormalised after 16 terms) and the
+//     three wave sums by thread 64, which adds s and writes / checks the tag.
+//     Same result as the Horner chain of crypto_aead_write / crypto_aead_read
+//     (monocypher.c:2858-2929): the sum IS that polynomial evaluated at r.
+//     Their hand-offs are LDS counter waits (grp_*), not workgroup barriers,
+//     and thread 64 raises the done word.
+//   wave 0: waits for the record's DMA (it issued it at detection), lets
+//     waves 1..3 go, then computes block 0 of nonce + 1 and its power ladder
+//     into the spare table nb -- the speculation for the next record runs
+//     while this one is served.
+template <bool DECRYPT_T, bool RT = false>
+__device__ void one_body_fast(const OneArgs &a, uint4 *lds, const SpecSlot *sp, const SpecBuf *cur,
+                              SpecBuf *nb_, uint32_t pmax_next, uint32_t *pre, uint32_t *sync) {
+  const bool DECRYPT = RT ? a.dec != 0u : DECRYPT_T;
   const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
   const uint32_t L = a.len, A = a.ad_len;
   const uint32_t na = (A + 15u) >> 4, nl = (L + 15u) >> 4;
@@ -596,27 +657,31 @@ __device__ void one_body_fast(const OneArgs &a, uint4 *lds, const SpecSlot *sp, 
   uint8_t *base = a.base;
   const uint32_t s_tag = na + nl, s_ok = s_tag + 1, s_w = s_ok + 1;
   const uint32_t npc = na + nl + (DECRYPT ? 1u : 0u);
-  // 1. request image -> LDS (one piece per thread: npc <= 257), unless the
-  // polling wave already issued it; block 0 of nonce + 1 meanwhile
-  if (!a.staged) one_stage_in(a.in_base, lay, npc, lds, t, kOneBlock);
-  if (wave == 0) spec_block0(pre, a.key.w, a.nonce + 1u, lane);
-  wait_vmem();
-  __syncthreads();
-  NOISE_ONE_STAMP(1);
-  // 2. block t: the product (m_t + 2^128) r^(P - t)
+  uint32_t *gc = sync;  // 0 at entry
+  if (wave == 0) {
+    wait_vmem();  // the DMA this wave issued at detection
+    grp_arrive(gc, lane);  // -> 1
+    spec_block0(pre, a.key.w, a.nonce + 1u, lane);
+    wave_sync_lds();
+    spec_ladder(nb_, pre, pmax_next, lane);
+    return;
+  }
+  const uint32_t u = t - 64u;
+  grp_wait(gc, 1u);
+  NOISE_FAST_STAMP(1);
   const uint32_t P = na + nl + 1u;
   F26 h;
 #pragma unroll
   for (int i = 0; i < 5; ++i) h.a[i] = 0u;
-  if (t < P) {
+  if (u < P) {
     uint4 m;
-    if (t < na) {
-      const uint32_t rem = A - 16u * t;
-      m = mask_bytes(lds[t], rem >= 16u ? 16 : (int)rem);
-    } else if (t < na + nl) {
-      const uint32_t p = t - na, rem = L - 16u * p;
+    if (u < na) {
+      const uint32_t rem = A - 16u * u;
+      m = mask_bytes(lds[u], rem >= 16u ? 16 : (int)rem);
+    } else if (u < na + nl) {
+      const uint32_t p = u - na, rem = L - 16u * p;
       const int nbytes = rem >= 16u ? 16 : (int)rem;
-      const uint32_t *ks = sp->ks + 16u * (1u + (p >> 2)) + 4u * (p & 3u);
+      const uint32_t *ks = cur->ks + 16u * (1u + (p >> 2)) + 4u * (p & 3u);
       const uint4 v = lds[na + p];
       if (!DECRYPT) {
         m = mask_bytes(make_uint4(v.x ^ ks[0], v.y ^ ks[1], v.z ^ ks[2], v.w ^ ks[3]), nbytes);
@@ -627,7 +692,7 @@ __device__ void one_body_fast(const OneArgs &a, uint4 *lds, const SpecSlot *sp, 
     } else {
       m = make_uint4(A, 0u, L, 0u);  // LE64(ad_len) || LE64(len)
     }
-    h = mul26(to26(m.x, m.y, m.z, m.w, 1u), pw_get(sp, P - t));
+    h = mul26(to26(m.x, m.y, m.z, m.w, 1u), pw_get(cur, P - u));
   }
   // < 2^26 + 2^9 per term: a row's 16 terms fit in 32 bits, renormalised
   // before the four rows are added
@@ -640,13 +705,14 @@ __device__ void one_body_fast(const OneArgs &a, uint4 *lds, const SpecSlot *sp, 
     lds[s_w + 2 * wave] = make_uint4(h.a[0], h.a[1], h.a[2], h.a[3]);
     lds[s_w + 2 * wave + 1] = make_uint4(h.a[4], 0u, 0u, 0u);
   }
-  __syncthreads();
-  if (t == 0) {
+  grp_arrive(gc, lane);  // -> 4
+  if (t == 64) {
+    grp_wait(gc, 4u);
     F26 H;
 #pragma unroll
     for (int i = 0; i < 5; ++i) H.a[i] = 0u;
 #pragma unroll
-    for (uint32_t w = 0; w < kOneBlock / 64; ++w) {
+    for (uint32_t w = 1; w < kOneBlock / 64; ++w) {
       const uint4 v0 = lds[s_w + 2 * w], v1 = lds[s_w + 2 * w + 1];
       H.a[0] += v0.x; H.a[1] += v0.y; H.a[2] += v0.z; H.a[3] += v0.w; H.a[4] += v1.x;
     }
@@ -664,34 +730,51 @@ __device__ void one_body_fast(const OneArgs &a, uint4 *lds, const SpecSlot *sp, 
       lds[s_ok] = make_uint4((w.x ^ tag[0]) | (w.y ^ tag[1]) | (w.z ^ tag[2]) | (w.w ^ tag[3]), 0u,
                              0u, 0u);
     }
+    grp_arrive1(gc);  // -> 5
   }
-  __syncthreads();
-  NOISE_ONE_STAMP(3);
-  // 3. LDS -> host image
+  grp_wait(gc, 5u);
+  NOISE_FAST_STAMP(3);
+  // LDS -> host image
   if (!DECRYPT) {
-    if (t <= nl) {  // ct pieces, then the tag
-      const uint4 v = lds[t < nl ? na + t : s_tag];
+    if (u <= nl) {  // ct pieces, then the tag
+      const uint4 v = lds[u < nl ? na + u : s_tag];
       const u32x4 w = {v.x, v.y, v.z, v.w};
-      st_sys16(base, lay.out + 16ull * t, w);
+      st_sys16(base, lay.out + 16ull * u, w);
     }
   } else {
     const bool ok = lds[s_ok].x == 0u;
-    if (ok && t < nl) {  // verified: plaintext out
-      const uint32_t rem = L - 16u * t;
-      const uint32_t *ks = sp->ks + 16u * (1u + (t >> 2)) + 4u * (t & 3u);
-      const uint4 v = lds[na + t];
+    if (ok && u < nl) {  // verified: plaintext out
+      const uint32_t rem = L - 16u * u;
+      const uint32_t *ks = cur->ks + 16u * (1u + (u >> 2)) + 4u * (u & 3u);
+      const uint4 v = lds[na + u];
       const uint4 o = mask_bytes(make_uint4(v.x ^ ks[0], v.y ^ ks[1], v.z ^ ks[2], v.w ^ ks[3]),
                                  rem >= 16u ? 16 : (int)rem);
       const u32x4 w = {o.x, o.y, o.z, o.w};
-      st_sys16(base, lay.out + 16ull * t, w);
+      st_sys16(base, lay.out + 16ull * u, w);
     }
-    if (t == 0)
+    if (t == 64)
       __hip_atomic_store(reinterpret_cast<uint32_t *>(base) + 1,
                          ok ? NOISE_GPU_REC_OK : NOISE_GPU_REC_BAD_MAC, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  NOISE_ONE_STAMP(4);
-  one_finish(a, lay, npc);
+  NOISE_FAST_STAMP(4);
+  // the request image zeroed (but for the seq words), every store drained,
+  // then the done word (as one_finish, over waves 1..3)
+  {
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    if (!a.n_inl && u < npc) st_sys16(a.in_base, lay.ad + 16ull * u, z);
+    req_wipe(a, u, kOneBlock - 64u);
+  }
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  grp_arrive(gc, lane);  // -> 8
+  if (t == 64) {
+    grp_wait(gc, 8u);
+    NOISE_FAST_STAMP(5);
+    __hip_atomic_store(reinterpret_cast<uint32_t *>(a.base), a.seq, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // 16 bytes of the request image, bypassing the caches (the host rewrites it
@@ -709,9 +792,23 @@ __device__ __forceinline__ u32x4 ld_sys16(const uint8_t *p) {
 #endif
 }
 
-// LDS: the staging image (one_lds_bytes(kOneMaxAd, 65535)), then the
-// speculation slots, then the request broadcast and the next block 0
-size_t resident_lds_bytes();
+// chunks lane and 64 + lane of the request image in one go (two loads in
+// flight, one wait)
+__device__ __forceinline__ void ld_sys16x2(const uint8_t *p, u32x4 &c0, u32x4 &c1) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("global_load_dwordx4 %0, %2, off sc0 sc1\n\t"
+               "global_load_dwordx4 %1, %2, off offset:1024 sc0 sc1\n\t"
+               "s_waitcnt vmcnt(0)"
+               : "=&v"(c0), "=&v"(c1) : "v"(p) : "memory");
+#else
+  c0 = ld_sys16(p);
+  c1 = ld_sys16(p + 1024);
+#endif
+}
+
+// LDS: the staging image (one_lds_bytes(kOneMaxAd, 65535)), the
+// speculation tables and slots, the request broadcast, the next block 0, the
+// group counter
 __global__ __launch_bounds__(kOneBlock) void k_aead_resident(uint8_t *req, uint8_t *base,
                                                              uint32_t last, uint64_t idle_ticks) {
 #if defined(NOISE_HIP_EMU)
@@ -719,30 +816,44 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_resident(uint8_t *req, uint8
 #else
   extern __shared__ uint4 lds[];
 #endif
-  const uint32_t t = threadIdx.x, lane = t & 63u;
+  const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
   const size_t stage = one_lds_bytes(kOneMaxAd, 65535u);
-  SpecSlot *slots = reinterpret_cast<SpecSlot *>(reinterpret_cast<uint8_t *>(lds) + stage);
+  SpecBuf *bufs = reinterpret_cast<SpecBuf *>(reinterpret_cast<uint8_t *>(lds) + stage);
+  SpecSlot *slots = reinterpret_cast<SpecSlot *>(bufs + kSpecBufs);
   uint32_t *cmd = reinterpret_cast<uint32_t *>(slots + kSpecSlots);
   uint32_t *pre = cmd + kResCmdWords;
-  if (t < kSpecSlots) slots[t].valid = 0u;
-  if (t == 0) pre[8] = 0u;
+  uint32_t *sync = pre + kResPreWords;  // [0] group counter, [1] spare table
+  if (t < kSpecSlots) {
+    slots[t].valid = 0u;
+    slots[t].buf = t;
+  }
+  if (t == 0) {
+    pre[8] = 0u;
+    sync[0] = 0u;
+    sync[1] = kSpecSlots;
+  }
   const OneRing *ring = reinterpret_cast<const OneRing *>(base + kOneRingOff);
   uint64_t t_last = __builtin_amdgcn_s_memrealtime();
-  uint32_t stamp = 0, nks = 16u;
+  uint32_t stamp = 0;
   __syncthreads();
   for (;;) {
-    if (t < 64) {  // wave 0 polls; lanes 0..3 own the request line's chunks
-      uint32_t ex = 0, polls = 0;
-      u32x4 c = {0u, 0u, 0u, 0u};
+    if (t < 64) {  // wave 0 polls chunks lane and 64 + lane (header: chunks 0..3)
+      uint32_t ex = 0, polls = 0, n_inl = 0;
+      u32x4 c = {0u, 0u, 0u, 0u}, c1 = {0u, 0u, 0u, 0u};
       for (;;) {
-        if (lane < 4) c = ld_sys16(req + 16u * lane);
+        ld_sys16x2(req + 16u * lane, c, c1);
         const uint32_t seq = (uint32_t)__shfl((int)c.x, 0);
         const uint64_t same = __ballot(lane < 4 && c.x == seq);
         if (seq != last && (same & 0xfull) == 0xfull) {
-#ifdef NOISE_ONE_TIMING
-          if (lane == 0) reinterpret_cast<uint64_t *>(base)[2] = __builtin_amdgcn_s_memrealtime();
-#endif
-          break;
+          // a complete header; an inline record must be complete too (every
+          // chunk carries this seq), else poll again
+          const uint32_t meta = (uint32_t)__shfl((int)c.y, 0);
+          n_inl = req_inline_chunks((meta >> 16) & 0x3fffu, meta & 0xffffu, (meta >> 30) & 1u);
+          const bool need0 = lane >= 4u && lane - 4u < n_inl, need1 = 60u + lane < n_inl;
+          if (__ballot((need0 && c.x != seq) || (need1 && c1.x != seq)) == 0ull) {
+            NOISE_ONE_STAMP(0);
+            break;
+          }
         }
         if ((++polls & 31u) == 0u &&
             (__hip_atomic_load(&ring->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
@@ -751,11 +862,23 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_resident(uint8_t *req, uint8
           break;
         }
       }
-      if (!ex) {  // this wave issues the record's DMA at once (the bodies only wait for it)
+      if (!ex) {
         const uint32_t meta = (uint32_t)__shfl((int)c.y, 0);
         const uint32_t L = meta & 0xffffu, A = (meta >> 16) & 0x3fffu, dec = (meta >> 30) & 1u;
-        if (A <= kOneMaxAd)
-          one_stage_in(req, one_layout(A, L), ((A + 15u) >> 4) + ((L + 15u) >> 4) + dec, lds, lane, 64u);
+        if (n_inl) {  // the inline image: chunk k's 12 bytes -> LDS bytes [12k, 12k + 12)
+          uint32_t *w = reinterpret_cast<uint32_t *>(lds);
+          if (lane >= 4u && lane - 4u < n_inl) {
+            const uint32_t k = lane - 4u;
+            w[3u * k] = c.y; w[3u * k + 1u] = c.z; w[3u * k + 2u] = c.w;
+          }
+          if (60u + lane < n_inl) {
+            const uint32_t k = 60u + lane;
+            w[3u * k] = c1.y; w[3u * k + 1u] = c1.z; w[3u * k + 2u] = c1.w;
+          }
+        } else if (A <= kOneMaxAd) {  // issue the record's DMA at once (the bodies only wait for it)
+          one_stage_in(req + kReqStageOff, one_layout(A, L),
+                       ((A + 15u) >> 4) + ((L + 15u) >> 4) + dec, lds, lane, 64u);
+        }
       }
       if (lane < 4) {
         cmd[4 * lane + 0] = c.x;
@@ -763,9 +886,14 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_resident(uint8_t *req, uint8
         cmd[4 * lane + 2] = c.z;
         cmd[4 * lane + 3] = c.w;
       }
-      if (lane == 0) cmd[0] = ex ? 0u : c.x;  // 0: leave
+      if (lane == 0) {
+        cmd[0] = ex ? 0u : c.x;  // 0: leave
+        cmd[16] = n_inl;
+      }
+      NOISE_ONE_STAMP(2);
     }
     __syncthreads();
+    const uint32_t n_inl = cmd[16];
     // chunk 0: seq, len | ad_len << 16 | decrypt << 30, nonce lo, hi;
     // chunks 1..3: seq + key words 0..2, 3..5, 6..7
     const uint32_t seq = cmd[0], meta = cmd[1];
@@ -774,60 +902,69 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_resident(uint8_t *req, uint8
     a.key.w[0] = cmd[5]; a.key.w[1] = cmd[6]; a.key.w[2] = cmd[7];
     a.key.w[3] = cmd[9]; a.key.w[4] = cmd[10]; a.key.w[5] = cmd[11];
     a.key.w[6] = cmd[13]; a.key.w[7] = cmd[14];
+    const uint32_t spare = sync[1];
     __syncthreads();  // cmd is rewritten only after every thread has read it
     if (seq == 0u) break;
     a.base = base;
-    a.in_base = req;
+    a.in_base = req + kReqStageOff;
+    a.req = req;
+    a.n_inl = n_inl;
     a.len = meta & 0xffffu;
     a.ad_len = (meta >> 16) & 0x3fffu;
     a.seq = seq;
     a.wipe_in = 1u;
     a.staged = 1u;
     const uint32_t dec = (meta >> 30) & 1u;
-    if (a.ad_len > kOneMaxAd) {  // the host never rings such a request
+    a.dec = dec;
+    if (a.ad_len > kOneMaxAd || a.len > kResidentMaxLen) {  // the host never rings such a request
       a.ad_len = 0;
+      a.len = 0;
       a.staged = 0u;
     }
-    // a speculation slot for exactly this (key, nonce)?
     const uint32_t na = (a.ad_len + 15u) >> 4, nl = (a.len + 15u) >> 4;
-    const uint32_t nb = (a.len + 63u) >> 6;
-    int hit = -1;
+    const uint32_t nb = (a.len + 63u) >> 6, P = na + nl + 1u;
+    // a speculation slot for exactly this (key, nonce)?  and the slot the
+    // next nonce goes to: the one holding this key, else the least recently
+    // used one
+    int hit = -1, dst = -1;
 #pragma unroll
     for (uint32_t i = 0; i < kSpecSlots; ++i) {
       const SpecSlot &sp = slots[i];
-      bool m = sp.valid && sp.nlo == (uint32_t)a.nonce && sp.nhi == (uint32_t)(a.nonce >> 32) &&
-               nb <= sp.nks;
+      bool k = sp.valid != 0u;
 #pragma unroll
-      for (int w = 0; w < 8; ++w) m = m && sp.key[w] == a.key.w[w];
-      if (m) hit = (int)i;
-    }
-    const bool fast = hit >= 0 && na + nl + 1u <= kSpecPowers;
-    if (fast) {
-      if (dec) one_body_fast<true>(a, lds, &slots[hit], pre);
-      else one_body_fast<false>(a, lds, &slots[hit], pre);
-    } else {
-      if (dec) one_body<true>(a, lds);
-      else one_body<false>(a, lds);
-    }
-    last = seq;
-    // speculate on the next nonce under this key: the slot that holds the
-    // key, else the least recently used one; as many keystream blocks as this
-    // record used (at least 16, at most 63)
-    int dst = -1;
-#pragma unroll
-    for (uint32_t i = 0; i < kSpecSlots; ++i) {
-      bool m = slots[i].valid != 0u;
-#pragma unroll
-      for (int w = 0; w < 8; ++w) m = m && slots[i].key[w] == a.key.w[w];
-      if (m) dst = (int)i;
+      for (int w = 0; w < 8; ++w) k = k && sp.key[w] == a.key.w[w];
+      if (k) dst = (int)i;
+      if (k && sp.nlo == (uint32_t)a.nonce && sp.nhi == (uint32_t)(a.nonce >> 32) && nb <= sp.nks &&
+          P <= sp.pmax)
+        hit = (int)i;
     }
     if (dst < 0) dst = !slots[0].valid ? 0 : !slots[1].valid ? 1 : (slots[0].stamp <= slots[1].stamp ? 0 : 1);
-    nks = nb < 16u ? 16u : (nb > kSpecBlocks - 1u ? kSpecBlocks - 1u : nb);
-    __syncthreads();  // every thread chose the same slot before it changes
-    spec_fill(&slots[dst], pre, a.key.w, a.nonce + 1u, ++stamp, nks);
-#ifdef NOISE_ONE_TIMING
-    if (t == 0) reinterpret_cast<uint64_t *>(base)[8] = __builtin_amdgcn_s_memrealtime();
-#endif
+    // the next speculation: as many keystream blocks as this record used (16
+    // to 63) and powers for a record of this size (80, 128 or 192 blocks)
+    const uint32_t nks = nb < 16u ? 16u : (nb > kSpecBlocks - 1u ? kSpecBlocks - 1u : nb);
+    const uint32_t pmax = P <= 80u ? 80u : (P <= 128u ? 128u : kFastMaxBlocks);
+    SpecBuf *nbuf = &bufs[spare];
+    NOISE_ONE_STAMP(7);
+    if (hit >= 0 && P <= kFastMaxBlocks) {
+      // waves 1..3 serve, wave 0 starts the next speculation meanwhile
+      one_body_fast<false, true>(a, lds, &slots[hit], &bufs[slots[hit].buf], nbuf, pmax, pre, sync);
+      __syncthreads();
+      if (wave != 0) spec_keystream(nbuf, a.key.w, a.nonce + 1u, nks, t);
+    } else {
+      one_body<false, true>(a, lds);
+      if (wave == 0) {  // block 0 of the next nonce, then its ladder, beside the keystream
+        spec_block0(pre, a.key.w, a.nonce + 1u, lane);
+        wave_sync_lds();
+        spec_ladder(nbuf, pre, pmax, lane);
+      } else {
+        spec_keystream(nbuf, a.key.w, a.nonce + 1u, nks, t);
+      }
+    }
+    last = seq;
+    __syncthreads();
+    spec_finish(&slots[dst], spare, nbuf, pre, sync, a.key.w, a.nonce + 1u, ++stamp, nks, pmax);
+    NOISE_ONE_STAMP(6);
+    NOISE_TS_FLUSH(base);  // this request's stamps, read by the host during the next one
 #pragma unroll
     for (int i = 0; i < 8; ++i) a.key.w[i] = 0u;
     t_last = __builtin_amdgcn_s_memrealtime();
@@ -835,7 +972,7 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_resident(uint8_t *req, uint8
   // leaving: no key or future keystream stays in this CU's LDS
   {
     uint32_t *w = reinterpret_cast<uint32_t *>(lds);
-    const size_t nw = (stage + kSpecSlots * sizeof(SpecSlot)) / 4 + kResCmdWords + kResPreWords;
+    const size_t nw = resident_lds_bytes() / 4;
     for (size_t i = t; i < nw; i += kOneBlock) w[i] = 0u;
   }
   __syncthreads();
@@ -849,10 +986,6 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_resident(uint8_t *req, uint8
 
 constexpr int kMaxAttrDev = 64;
 
-size_t resident_lds_bytes() {
-  return one_lds_bytes(kOneMaxAd, 65535u) + kSpecSlots * sizeof(SpecSlot) +
-         4u * (kResCmdWords + kResPreWords);
-}
 
 static hipError_t one_attr() {
   // > 64 KiB of dynamic LDS needs the opt-in, which is per device: set once
@@ -902,6 +1035,9 @@ hipError_t launch_aead_one(bool decrypt, const uint32_t key[8], uint64_t nonce,
   a.seq = seq;
   a.wipe_in = 0u;
   a.staged = 0u;
+  a.req = nullptr;
+  a.n_inl = 0u;
+  a.dec = decrypt ? 1u : 0u;
   const size_t lds = one_lds_bytes(ad_len, len);
   if (decrypt)
     hipLaunchKernelGGL((k_aead_one<true>), dim3(1), dim3(kOneBlock), lds, stream, a);

@@ -207,6 +207,8 @@ void launch(K kernel, dim3 g, dim3 b, A... args) {
 #define __HIP_MEMORY_SCOPE_SYSTEM 0
 #define __hip_atomic_store(p, v, order, scope) __atomic_store_n((p), (v), __ATOMIC_SEQ_CST)
 #define __hip_atomic_load(p, order, scope) __atomic_load_n((p), __ATOMIC_SEQ_CST)
+#define __hip_atomic_fetch_add(p, v, order, scope) __atomic_fetch_add((p), (v), __ATOMIC_SEQ_CST)
+#define __HIP_MEMORY_SCOPE_WORKGROUP 0
 // s_memrealtime: a 100 MHz constant clock
 #define __builtin_amdgcn_s_memrealtime()                                         \
   ((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(              \

@@ -49,7 +49,7 @@ int main() {
         }
         const auto t1 = std::chrono::steady_clock::now();
         (void)hipStreamSynchronize(st);
-        const uint64_t *ts = reinterpret_cast<const uint64_t *>(h) + 2;
+        const uint64_t *ts = reinterpret_cast<const uint64_t *>(h + kOneTsOff);
         for (int i = 0; i < 5; ++i) ph[i].push_back((ts[i + 1] - ts[i]) * 0.01);
         tot.push_back((ts[5] - ts[0]) * 0.01);
         wall.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());

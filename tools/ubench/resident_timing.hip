@@ -46,17 +46,29 @@ int main(int argc, char **argv) {
   std::printf("# %s request image; us: detect->data  data->tag  tag->stores  stores->done | spec "
               "| prev done -> detect | host wall per call\n", hostreq ? "host" : "fine-grained");
   std::vector<uint8_t> out(70000);
-  for (uint32_t L : {64u, 1024u, 4032u, 16384u}) {
+  for (uint32_t L : {64u, 1024u, 1472u, 3000u, 16384u}) {
     const OneLayout lay = one_layout(0, L);
-    std::vector<double> ph[4], spec, idle, wall;
+    std::vector<double> ph[4], spec, idle, wall, unp, hitv;
     uint64_t prev_spec_end = 0;
     for (int it = 0; it < 200; ++it) {
       std::vector<uint8_t> pt(L);
       for (uint32_t i = 0; i < L; ++i) pt[i] = (uint8_t)(i * 7 + it);
-      const uint32_t s = ++seq;
       const auto t0 = std::chrono::steady_clock::now();
-      std::memcpy(hq + lay.in, pt.data(), L);
+      const uint32_t n_inl = req_inline_chunks(0, L, false);
+      if (n_inl) {
+        std::vector<uint8_t> im(12 * n_inl + 16, 0);
+        std::memcpy(im.data(), pt.data(), L);
+        for (uint32_t k = 0; k < n_inl; ++k) {
+          uint32_t w[3];
+          std::memcpy(w, im.data() + 12 * k, 12);
+          _mm_store_si128(reinterpret_cast<__m128i *>(hq) + 4 + k,
+                          _mm_setr_epi32((int)(seq + 1), (int)w[0], (int)w[1], (int)w[2]));
+        }
+      } else {
+        std::memcpy(hq + kReqStageOff + lay.in, pt.data(), L);
+      }
       _mm_sfence();
+      const uint32_t s = ++seq;
       __m128i *q = reinterpret_cast<__m128i *>(hq);
       _mm_store_si128(q + 1, _mm_setr_epi32((int)s, (int)key[0], (int)key[1], (int)key[2]));
       _mm_store_si128(q + 2, _mm_setr_epi32((int)s, (int)key[3], (int)key[4], (int)key[5]));
@@ -71,33 +83,31 @@ int main(int argc, char **argv) {
       if (*done != s) { std::printf("no answer\n"); return 3; }
       std::memcpy(out.data(), h + lay.out, L + 16);
       const auto t1 = std::chrono::steady_clock::now();
-      const volatile uint64_t *ts = reinterpret_cast<const volatile uint64_t *>(h) + 2;
-      // [0] detect [1] data [3] stores (2 is unused by the fast path) [4] before flag [5] done [6] spec end (previous)
-      const uint64_t t_det = ts[0], t_data = ts[1], t_tag = ts[3], t_st = ts[4], t_done = ts[5];
+      // the stamps now in the done line are the PREVIOUS request's (the
+      // kernel copies them out after its speculation, off the critical path):
+      // [0] detect [1] data in LDS [3] tag [4] stores issued [5] done [6] spec end
+      const volatile uint64_t *ts = reinterpret_cast<const volatile uint64_t *>(h + kOneTsOff);
+      const uint64_t t_det = ts[0], t_data = ts[1], t_tag = ts[3], t_st = ts[4], t_done = ts[5],
+                     t_spec = ts[6], t_unp = ts[2], t_hit = ts[7];
+      if (it >= 10) { unp.push_back((t_unp - t_det) * 0.01); hitv.push_back((t_hit - t_det) * 0.01); }
       if (it >= 10) {
         ph[0].push_back((t_data - t_det) * 0.01);
         ph[1].push_back((t_tag - t_data) * 0.01);
         ph[2].push_back((t_st - t_tag) * 0.01);
         ph[3].push_back((t_done - t_st) * 0.01);
+        spec.push_back((t_spec - t_done) * 0.01);
+        if (prev_spec_end) idle.push_back(((double)(int64_t)(t_det - prev_spec_end)) * 0.01);
         wall.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
       }
-      // every 10th call: wait for this request's speculation to end, time it
-      if (it % 10 == 5) {
-        std::this_thread::sleep_for(std::chrono::microseconds(100));
-        spec.push_back((ts[6] - t_done) * 0.01);
-        prev_spec_end = 0;
-      } else {
-        if (prev_spec_end && it >= 10) idle.push_back(((double)(int64_t)(t_det - prev_spec_end)) * 0.01);
-        prev_spec_end = t_done;
-      }
+      prev_spec_end = t_done;  // this (previous) request's done -> the next one's detect
     }
     auto med = [](std::vector<double> v) {
       if (v.empty()) return -1.0;
       std::sort(v.begin(), v.end());
       return v[v.size() / 2];
     };
-    std::printf("L %5u: %.2f %.2f %.2f %.2f | %.2f | %.2f | %.2f\n", L, med(ph[0]), med(ph[1]),
-                med(ph[2]), med(ph[3]), med(spec), med(idle), med(wall));
+    std::printf("L %5u: %.2f %.2f %.2f %.2f | %.2f | %.2f | %.2f   (detect->unpacked %.2f, ->slot chosen %.2f)\n", L, med(ph[0]), med(ph[1]),
+                med(ph[2]), med(ph[3]), med(spec), med(idle), med(wall), med(unp), med(hitv));
   }
   reinterpret_cast<OneRing *>(h + kOneRingOff)->stop = 1u;
   (void)hipStreamSynchronize(st);

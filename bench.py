@@ -321,11 +321,14 @@ def config1(orc=None):
     tool = os.path.join(ROOT, "noise-cpp_amd", "bin", "config1_bench")
     if not os.path.exists(tool):
         return {"error": "noise-cpp_amd/bin/config1_bench not built"}
-    p = subprocess.run([tool, "1000", "1024"], capture_output=True, text=True, timeout=300)
-    if p.returncode != 0:
-        return {"error": "config1_bench failed: " + p.stderr[-500:]}
-    build = json.loads(p.stdout.strip().splitlines()[-1])
-    out = {"build": build}
+    # resident: the opt-in latency mode (noise_gpu_set_resident: one resident
+    # workgroup, no launch per record); launch: one kernel launch per record
+    out = {}
+    for mode in ("resident", "launch"):
+        p = subprocess.run([tool, "1000", "1024", mode], capture_output=True, text=True, timeout=300)
+        if p.returncode != 0:
+            return {"error": "config1_bench %s failed: %s" % (mode, p.stderr[-500:])}
+        out["build" if mode == "resident" else "build_launch"] = json.loads(p.stdout.strip().splitlines()[-1])
     if orc is None:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib

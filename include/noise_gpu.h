@@ -304,17 +304,32 @@ int noise_gpu_rekey_host(uint8_t h_key[32]);
 /* Resident latency mode (opt-in) for the single-record entry points above,
  * for the calling thread on its current device.  on = 1: instead of one
  * kernel launch per record, ONE workgroup stays on the GPU and serves the
- * thread's records through the host-mapped staging image: the host writes
- * the record and a request line (key, nonce, lengths) and bumps a doorbell
- * the workgroup polls; completion is the same done word.  The workgroup
- * leaves on its own after idle_us microseconds without a request (0 = the
- * default, 20000; at most 10 s), is relaunched by the next request, and is
- * stopped by on = 0, noise_gpu_thread_release, thread exit and library
- * unload.  While it runs it holds one CU and ~74 KB of its LDS, and a
- * device-wide synchronisation (hipDeviceSynchronize) waits for it to idle
- * out.  Results, hygiene and error behaviour are those of the launch path.
- * Records with more than 8192 bytes of AD or more than 65535 bytes take the
- * staged path either way. */
+ * thread's records of up to 4032 bytes (<= 8192 bytes of AD):
+ *   - the host writes each request into a request image in fine-grained
+ *     device memory through the PCIe BAR: 16-byte chunks {seq, 12 bytes}
+ *     carrying the key, nonce, lengths and -- for a staged image of up to
+ *     1488 bytes -- the AD / record themselves, so the poll that finds the
+ *     request has its data (larger ones follow by DMA);
+ *   - output, status and the done word come back through the host-mapped
+ *     staging image as in the launch path;
+ *   - after answering (key, n) the workgroup precomputes (key, n + 1): its
+ *     keystream and the Poly1305 powers r..r^192, two such slots (a session's
+ *     two directions), so consecutive records of a CipherState are answered
+ *     with one product per 16-byte block.
+ * Records above 4032 bytes take a kernel launch on a second stream.  The
+ * workgroup leaves on its own after idle_us microseconds without a request
+ * (0 = the default, 20000; at most 10 s), is relaunched by the next request,
+ * and is stopped by on = 0 (which also frees the request image),
+ * noise_gpu_thread_release, thread exit and library unload; on the way out it
+ * zeroes its LDS (speculated keystream, key copies).  While it runs it holds
+ * one CU and ~105 KB of its LDS, and a device-wide synchronisation
+ * (hipDeviceSynchronize) waits for it to idle out.  A request it does not
+ * answer within 10 s fails with NOISE_GPU_E_HIP.  Results, hygiene (the
+ * request image is zeroed, but for four sequence words, before the done word)
+ * and error behaviour are those of the launch path.  NOISE_GPU_RESIDENT_REQ=
+ * host puts the request image in host-mapped memory instead (polled over
+ * PCIe).  Records with more than 8192 bytes of AD or more than 65535 bytes
+ * take the staged path either way. */
 int noise_gpu_set_resident(int on, uint32_t idle_us);
 
 /* Descriptor batch between HOST buffers (synchronous): the key table

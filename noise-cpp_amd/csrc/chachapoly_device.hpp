@@ -11,10 +11,15 @@
 // record, with no r-power precomputation (a k-lane split of one record's
 // Poly1305 would need r^2..r^k per record, +30-120 % Poly work).
 //
-// Arithmetic references (what is computed, not how):
-//   ChaCha20 quarter-round / 20 rounds   monocypher.c:169-200
-//   keystream feed-forward, counter      monocypher.c:219-253
-//   Poly1305 clamp / block / final       monocypher.c:366-440
+// Arithmetic references:
+//   ChaCha20 quarter-round / 20 rounds   monocypher.c:169-200 (what is computed)
+//   keystream feed-forward, counter      monocypher.c:219-253 (what is computed)
+//   Poly1305 clamp                        monocypher.c:366-375
+//   Poly1305 block (poly_block)           monocypher.c:314-357 -- also the
+//     formulation: the radix-2^32 limbs, rr_j = r_j + (r_j >> 2), the
+//     five-term column sums and the fold of the bits above 2^130 (the carry
+//     handling here is this build's own: full carries at the add)
+//   Poly1305 final (poly_final)           monocypher.c:426-438 (formulation too)
 //   AEAD layout ad|pad|ct|pad|lens       monocypher.c:2858-2873
 //   Noise nonce 0^32 || LE64(n)          noise.cpp:207-215
 #pragma once

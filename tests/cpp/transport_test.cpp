@@ -304,6 +304,7 @@ static int run_bench(const std::string &mode, int S, long M, std::size_t len, in
   using clk = std::chrono::steady_clock;
   std::uint64_t sum = 0;
   double secs[2] = {0, 0};
+  double phase[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};  // submit_batch, flush, wait, copy_out
   bytes ctall((std::size_t)M * (len + 16)), ptall(threads > 1 ? (std::size_t)M * len : 0);
   // long-lived objects, as in a server: built (pinned slots, key upload)
   // outside the timed region
@@ -343,7 +344,10 @@ static int run_bench(const std::string &mode, int S, long M, std::size_t len, in
           while (q.size() > keep) {
             auto [t, f] = q.front();
             q.pop_front();
+            const auto w0 = clk::now();
             const nt::Pipeline::Batch b = p.wait(t);
+            const auto w1 = clk::now();
+            phase[d][2] += std::chrono::duration<double>(w1 - w0).count();
             // results consumed: every message copied out (as a send() would), in parallel
             for (std::size_t j = 0; j < b.size(); ++j)
               dst[j] = dec ? ptall.data() + (f + j) * len : ctall.data() + (f + j) * (len + 16);
@@ -351,14 +355,19 @@ static int run_bench(const std::string &mode, int S, long M, std::size_t len, in
             if (dec)
               for (std::size_t j = 0; j < b.size(); ++j)
                 if (!b.ok(j)) throw std::runtime_error("bench: decrypt failed");
+            phase[d][3] += std::chrono::duration<double>(clk::now() - w1).count();
           }
         };
         long i = 0, first = 0;
         while (i < M) {
+          const auto s0 = clk::now();
           const std::size_t k = p.submit_batch(msgs.data() + i, (std::size_t)(M - i));
+          const auto s1 = clk::now();
+          phase[d][0] += std::chrono::duration<double>(s1 - s0).count();
           i += (long)k;
           if (i < M) {
             q.push_back({p.flush(), first});
+            phase[d][1] += std::chrono::duration<double>(clk::now() - s1).count();
             first = i;
             take(1);
           }
@@ -403,8 +412,13 @@ static int run_bench(const std::string &mode, int S, long M, std::size_t len, in
   }
   const double gib = (double)M * len * 2 / (1u << 30);  // two timed passes per direction
   std::printf("{\"mode\": \"%s\", \"copy_threads\": %d, \"sessions\": %d, \"messages\": %ld, "
-              "\"len\": %zu, \"encrypt_gib_s\": %.2f, \"decrypt_gib_s\": %.2f, \"checksum\": %llu}\n",
-              mode.c_str(), threads, S, M, len, gib / secs[0], gib / secs[1], (unsigned long long)sum);
+              "\"len\": %zu, \"encrypt_gib_s\": %.2f, \"decrypt_gib_s\": %.2f, "
+              "\"phases_ms\": {\"encrypt\": [%.1f, %.1f, %.1f, %.1f], \"decrypt\": [%.1f, %.1f, %.1f, %.1f], "
+              "\"order\": \"submit_batch, flush, wait, copy_out + status check (batched mode; all passes)\"}, "
+              "\"checksum\": %llu}\n",
+              mode.c_str(), threads, S, M, len, gib / secs[0], gib / secs[1], phase[0][0] * 1e3,
+              phase[0][1] * 1e3, phase[0][2] * 1e3, phase[0][3] * 1e3, phase[1][0] * 1e3, phase[1][1] * 1e3,
+              phase[1][2] * 1e3, phase[1][3] * 1e3, (unsigned long long)sum);
   return 0;
 }
 

@@ -174,6 +174,10 @@ class Pipeline {
   bool keys_uploaded_ = false;
   struct CopyPool;
   std::unique_ptr<CopyPool> pool_;
+  // submit_batch's parallel bookkeeping: per copy thread, its messages' count
+  // per session and byte totals (scratch kept across calls)
+  std::vector<std::uint32_t> sess_cnt_;
+  std::size_t submit_serial(const Message *messages, std::size_t n);
 };
 
 }  // namespace noise::transport

@@ -356,7 +356,7 @@ bool Pipeline::submit(std::size_t s, const std::uint8_t *msg, std::size_t len) {
   return true;
 }
 
-std::size_t Pipeline::submit_batch(const Message *messages, std::size_t n) {
+std::size_t Pipeline::submit_serial(const Message *messages, std::size_t n) {
   const bool dec = dir_ == Direction::Decrypt;
   Slot &sl = *slots_[fill_];
   // 1. bookkeeping in order (cheap): nonces, offsets, descriptors
@@ -397,6 +397,134 @@ std::size_t Pipeline::submit_batch(const Message *messages, std::size_t n) {
   sl.nrec += k;
   sl.in_used = in_used;
   sl.out_used = out_used;
+  return k;
+}
+
+// The bookkeeping of submit_batch in parallel as well as the copies (the
+// serial loop above cost ~10 ns per message: at 256-byte messages it bound
+// the Pipeline below the CPU).  Over the copy pool's T contiguous chunks of
+// the messages that fit:
+//   1. each thread finds its chunk's first refused message and its byte
+//      total, and counts its messages per session;
+//   2. the caller cuts the batch at the slot's record / byte capacity and the
+//      first refused message, and gives every chunk its byte offsets and, per
+//      session, its first nonce (the session's nonce + the earlier chunks'
+//      counts) -- what consecutive submit() calls would have assigned;
+//   3. each thread writes its descriptors and copies its messages.
+// Falls back to the serial walk for few messages, a single thread, very many
+// sessions (the counters are T x sessions) or a batch reaching a session's
+// nonce limit (the exact exception order is the serial walk's).
+std::size_t Pipeline::submit_batch(const Message *messages, std::size_t n) {
+  const bool dec = dir_ == Direction::Decrypt;
+  Slot &sl = *slots_[fill_];
+  const std::size_t T = (std::size_t)pool_->nthr, S = nonces_.size();
+  const std::size_t n0 = std::min(n, opt_.slot_records - sl.nrec);
+  if (T == 1 || n0 < 4096 || S * T > (std::size_t(1) << 22)) return submit_serial(messages, n);
+  auto in_len_of = [](std::size_t len) { return align16(len); };
+  auto out_len_of = [dec](std::size_t len) { return dec ? align16(len - 16) : align16(len + 16); };
+  auto refused = [&](const Message &m) {
+    return m.session >= S || (dec ? (m.len < 16 || m.len > kMaxMessage) : m.len + 16 > kMaxMessage);
+  };
+  // the pool's chunk c of [0, len) is [len c / T, len (c + 1) / T) (one
+  // chunk below 64 messages); its index from its first message
+  auto chunk_of = [T](std::size_t lo, std::size_t len) {
+    return len < 64 ? std::size_t(0) : (lo * T + len - 1) / len;
+  };
+  // 1. per chunk: the first refused message, the input bytes before it
+  std::vector<std::size_t> bad(T, n0), bytes(T, 0);
+  pool_->run(n0, [&](std::size_t lo, std::size_t hi) {
+    const std::size_t c = chunk_of(lo, n0);
+    std::size_t b = 0;
+    for (std::size_t i = lo; i < hi; ++i) {
+      if (refused(messages[i])) {
+        bad[c] = i;
+        break;
+      }
+      b += in_len_of(messages[i].len);
+    }
+    bytes[c] = b;
+  });
+  std::size_t k = n0;
+  for (std::size_t c = 0; c < T; ++c) k = std::min(k, bad[c]);
+  if (k == 0) return submit_serial(messages, n);  // throws exactly as submit() would
+  {  // the byte capacity: walk the chunk where the running total passes it
+    std::size_t used = sl.in_used;
+    for (std::size_t c = 0; c < T; ++c) {
+      const std::size_t lo = n0 * c / T, end = n0 * (c + 1) / T, hi = std::min(k, end);
+      if (lo >= hi) break;
+      if (hi == end && used + bytes[c] <= opt_.slot_bytes) {
+        used += bytes[c];
+        continue;
+      }
+      std::size_t i = lo;
+      for (; i < hi; ++i) {
+        const std::size_t l = in_len_of(messages[i].len);
+        if (used + l > opt_.slot_bytes) break;
+        used += l;
+      }
+      k = i;
+      break;
+    }
+  }
+  if (k == 0) return 0;  // the slot is full: flush() and call again
+  // 2. per chunk of [0, k): its messages per session and its bytes
+  sess_cnt_.assign(T * S, 0u);
+  std::vector<std::size_t> in_b(T + 1, 0), out_b(T + 1, 0);
+  pool_->run(k, [&](std::size_t lo, std::size_t hi) {
+    const std::size_t c = chunk_of(lo, k);
+    std::uint32_t *cnt = sess_cnt_.data() + c * S;
+    std::size_t bi = 0, bo = 0;
+    for (std::size_t i = lo; i < hi; ++i) {
+      ++cnt[messages[i].session];
+      bi += in_len_of(messages[i].len);
+      bo += out_len_of(messages[i].len);
+    }
+    in_b[c + 1] = bi;
+    out_b[c + 1] = bo;
+  });
+  in_b[0] = sl.in_used;
+  out_b[0] = sl.out_used;
+  for (std::size_t c = 0; c < T; ++c) {
+    in_b[c + 1] += in_b[c];
+    out_b[c + 1] += out_b[c];
+  }
+  // each chunk's first nonce per session (the session's nonce + the earlier
+  // chunks' counts); a batch that would reach a nonce limit takes the serial
+  // walk, which throws at exactly the message submit() would
+  constexpr std::uint64_t kLimit = std::numeric_limits<std::uint64_t>::max() - 1;
+  std::vector<std::uint64_t> first(T * S), after(S);
+  for (std::size_t s = 0; s < S; ++s) {
+    std::uint64_t run = nonces_[s];
+    for (std::size_t c = 0; c < T; ++c) {
+      const std::uint32_t m = sess_cnt_[c * S + s];
+      if (kLimit - run < m) return submit_serial(messages, n);
+      first[c * S + s] = run;
+      run += m;
+    }
+    after[s] = run;
+  }
+  // 3. descriptors and copies
+  const std::size_t base = sl.nrec;
+  pool_->run(k, [&](std::size_t lo, std::size_t hi) {
+    const std::size_t c = chunk_of(lo, k);
+    std::uint64_t *nx = first.data() + c * S;
+    std::size_t io = in_b[c], oo = out_b[c];
+    noise_gpu_record *recs = sl.recs();
+    for (std::size_t i = lo; i < hi; ++i) {
+      const Message &m = messages[i];
+      recs[base + i] = noise_gpu_record{io, oo, nx[m.session]++, 0,
+                                        (std::uint32_t)(dec ? m.len - 16 : m.len), 0,
+                                        (std::uint32_t)m.session, 0};
+      if (m.len) stream_copy(sl.h + o_in_ + io, m.data, m.len);
+      io += in_len_of(m.len);
+      oo += out_len_of(m.len);
+    }
+    stream_fence();  // visible to the H2D copy flush() issues
+  });
+  nonces_.swap(after);  // decrypt: advances whatever the tags say (noise.cpp:421)
+  sl.nrec += k;
+  sl.in_used = in_b[T];
+  sl.out_used = out_b[T];
   return k;
 }
 

@@ -160,15 +160,20 @@ static int run_pipeline(int S, int M, std::uint64_t seed) {
 // Pipeline::submit_batch / copy_out (4 copy threads): ragged chunks of
 // messages (1..300, crossing slot boundaries), ciphertexts vs the oracle,
 // then decrypt back through batches with tampered records.
-static int run_pipeline_batch(int S, int M, std::uint64_t seed) {
+// slot_records >= 4096 with several copy threads takes submit_batch's
+// parallel bookkeeping (chunked session counts / nonce scan); the default
+// tiny slots its serial walk
+static int run_pipeline_batch(int S, int M, std::uint64_t seed, std::size_t slot_records = 97,
+                              std::size_t slot_bytes = 256 << 10, std::size_t maxlen = 3000,
+                              int maxbatch = 300) {
   std::mt19937_64 rng(seed);
   int fails = 0;
   auto check = [&](bool c, const char *what, long i) {
     if (!c && fails++ < 20) std::printf("FAIL %s (%ld)\n", what, i);
   };
   nt::Pipeline::Options o;
-  o.slot_bytes = 256 << 10;
-  o.slot_records = 97;
+  o.slot_bytes = slot_bytes;
+  o.slot_records = slot_records;
   o.depth = 3;
   o.copy_threads = 4;
   nt::Pipeline enc(nt::Pipeline::Direction::Encrypt, o), dec(nt::Pipeline::Direction::Decrypt, o);
@@ -186,7 +191,7 @@ static int run_pipeline_batch(int S, int M, std::uint64_t seed) {
   std::vector<bytes> pt(M), ct(M), back(M);
   std::vector<nt::Pipeline::Message> msgs(M);
   for (int i = 0; i < M; ++i) {
-    pt[i].resize(rng() % 29 == 0 ? 65519 : rng() % 3000);
+    pt[i].resize(rng() % 29 == 0 ? 65519 : rng() % maxlen);
     for (auto &b : pt[i]) b = (std::uint8_t)rng();
     msgs[i] = {(std::size_t)(rng() % S), pt[i].data(), pt[i].size()};
   }
@@ -209,7 +214,7 @@ static int run_pipeline_batch(int S, int M, std::uint64_t seed) {
     };
     int i = 0, first = 0;
     while (i < M) {
-      const int want = std::min<int>(M - i, 1 + (int)(rng() % 300));
+      const int want = std::min<int>(M - i, 1 + (int)(rng() % maxbatch));
       const std::size_t k = p.submit_batch(msgs.data() + i, (std::size_t)want);
       i += (int)k;
       if (k < (std::size_t)want) {
@@ -426,8 +431,13 @@ int main(int argc, char **argv) {
   if (argc > 1 && std::string(argv[1]) == "pipeline")
     return run_pipeline(std::atoi(argv[2]), std::atoi(argv[3]), std::strtoull(argv[4], nullptr, 0));
   if (argc > 1 && std::string(argv[1]) == "keyrace") return run_keyrace(std::atoi(argv[2]));
-  if (argc > 1 && std::string(argv[1]) == "pipeline_batch")
+  if (argc > 1 && std::string(argv[1]) == "pipeline_batch") {
+    if (argc > 8)  // slot_records slot_bytes maxlen maxbatch
+      return run_pipeline_batch(std::atoi(argv[2]), std::atoi(argv[3]), std::strtoull(argv[4], nullptr, 0),
+                                std::strtoull(argv[5], nullptr, 0), std::strtoull(argv[6], nullptr, 0),
+                                std::strtoull(argv[7], nullptr, 0), std::atoi(argv[8]));
     return run_pipeline_batch(std::atoi(argv[2]), std::atoi(argv[3]), std::strtoull(argv[4], nullptr, 0));
+  }
   if (argc > 1 && std::string(argv[1]) == "bench")
     return run_bench(argv[2], std::atoi(argv[3]), std::atol(argv[4]), std::strtoul(argv[5], nullptr, 0),
                      argc > 6 ? std::atoi(argv[6]) : 1);

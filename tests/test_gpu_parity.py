@@ -599,13 +599,18 @@ def test_transport_pipeline(sessions, messages, seed):
     assert "ok (0 failures)" in r.stdout
 
 
-@pytest.mark.parametrize("sessions,messages,seed", [(60, 2500, 5)])
-def test_transport_pipeline_batched_copies(sessions, messages, seed):
+@pytest.mark.parametrize("sessions,messages,seed,big", [(60, 2500, 5, False), (700, 40000, 6, True),
+                                                       (3, 30000, 7, True)])
+def test_transport_pipeline_batched_copies(sessions, messages, seed, big):
     """Pipeline::submit_batch / copy_out with 4 copy threads: ragged batches
     crossing slot boundaries, ciphertexts vs the oracle, nonce accounting,
-    decrypt round trip with tampered records rejected."""
+    decrypt round trip with tampered records rejected.  big: slots of 8192
+    records / 2 MiB and batches of up to 20000 messages (the parallel
+    bookkeeping: per-chunk session counts, the nonce scan, slots cut by the
+    record and the byte capacity; 3 sessions: long runs per session)."""
     exe = os.path.join(noise_amd.ROOT, "noise-cpp_amd", "bin", "transport_test")
-    r = subprocess.run([exe, "pipeline_batch", str(sessions), str(messages), str(seed)],
+    extra = ["8192", str(2 << 20), "600", "20000"] if big else []
+    r = subprocess.run([exe, "pipeline_batch", str(sessions), str(messages), str(seed)] + extra,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "ok (0 failures)" in r.stdout

@@ -153,6 +153,14 @@ int noise_gpu_decrypt_records(const uint8_t *d_keys, uint32_t nkeys,
  * session teardown.  The host-buffer entry points below wipe it themselves. */
 int noise_gpu_scratch_wipe(void *stream);
 
+/* Zero and free the records scratch and the companion stream the descriptor
+ * path cached for (current device, `stream`); synchronises `stream` first.
+ * Call it before destroying a stream of your own that the descriptor
+ * functions were called on (noise_gpu_ctx_destroy does it for the context's
+ * streams); otherwise both stay allocated until the library is unloaded.
+ * A stream with nothing cached is a no-op. */
+int noise_gpu_scratch_release(void *stream);
+
 /* ---- device-resident many-session batches (BASELINE config 3) ---------
  * nrec records of `len` plaintext bytes, record i under key row
  * d_keys[d_key_idx[i]] (a [nkeys][32] table, 16-byte aligned) with Noise

@@ -682,6 +682,13 @@ int noise_gpu_scratch_wipe(void *stream) {
   return NOISE_GPU_OK;
 }
 
+int noise_gpu_scratch_release(void *stream) {
+  int rc = check_device();
+  if (rc) return rc;
+  HIP_TRY(noise_amd::records_scratch_release((hipStream_t)stream));
+  return NOISE_GPU_OK;
+}
+
 int noise_gpu_fill_synthetic(uint8_t *d_dst, uint64_t offset, uint64_t nbytes,
                              uint64_t seed, void *stream) {
   if (nbytes == 0) return NOISE_GPU_OK;

@@ -94,7 +94,11 @@ class Batcher {
 //   auto b = p.wait(tickets.front());   // b.data(i) / b.length(i) / b.ok(i)
 // A Batch view stays valid until its slot is refilled, i.e. until `depth - 1`
 // further flushes; flush() blocks only when the slot it moves on to is still
-// in flight (back-pressure).  Session keys are uploaded to a device key table
+// in flight (back-pressure).  With Options::launch_thread the slot's HIP work
+// is enqueued by a launcher thread, so flush() returns at once and the
+// enqueue overlaps the caller's copies; an enqueue error is rethrown by the
+// next flush() / wait().  The launcher uses the device current when the
+// Pipeline was built.  Session keys are uploaded to a device key table
 // once, when the session is added.  One thread drives a Pipeline (like
 // CipherState); submit_batch / copy_out fan the byte copies out to an
 // internal pool of Options::copy_threads threads.
@@ -103,10 +107,13 @@ class Pipeline {
   using Direction = Batcher::Direction;
   struct Options {
     std::size_t slot_bytes = std::size_t(32) << 20;  // message bytes per slot
-    std::size_t slot_records = std::size_t(1) << 16; // messages per slot
-    int depth = 3;                                   // slots in the ring
+    std::size_t slot_records = std::size_t(1) << 17; // messages per slot (48-B descriptors)
+    int depth = 4;  // slots in the ring: one filling, depth - 2 in flight while
+                    // the oldest is consumed (a slot's copies take ~1.3 ms at 32 MiB)
     int copy_threads = 1;  // host threads copying messages in / results out
                            // (submit_batch, copy_out); 1 = the caller only
+    bool launch_thread = true;  // flush() hands a slot's HIP enqueue (copies,
+                                // kernels, event) to a thread of its own
   };
   struct Message {
     std::size_t session;
@@ -161,6 +168,12 @@ class Pipeline {
   struct Slot;
   void sync_all();
   void grow_keys();
+  struct LaunchJob;
+  void enqueue(const LaunchJob &j);  // the slot's HIP work, in stream order
+  void wait_enqueued(Slot &sl);      // the launcher has issued sl's work
+  struct Launcher;
+  std::unique_ptr<Launcher> launcher_;
+  int dev_ = 0;
   Direction dir_;
   Options opt_;
   std::size_t o_in_ = 0, o_out_ = 0, o_st_ = 0, slot_total_ = 0;

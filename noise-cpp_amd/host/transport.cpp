@@ -4,6 +4,8 @@
 
 #include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <exception>
 #include <functional>
 #include <limits>
 #include <mutex>
@@ -235,10 +237,33 @@ struct Pipeline::Slot {
   std::size_t nrec = 0, in_used = 0, out_used = 0;
   std::uint64_t ticket = 0;
   bool in_flight = false;
+  bool enqueued = true;  // the launcher has issued its work (Launcher::mu)
   noise_gpu_record *recs() { return reinterpret_cast<noise_gpu_record *>(h); }
 };
 
+// What flush() hands over: the slot and the key rows it needs uploaded,
+// snapshotted on the caller's thread (add_session() may append rows after).
+struct Pipeline::LaunchJob {
+  Slot *sl;
+  std::size_t key_lo, nkeys;
+};
+
+// The launcher thread.  A flush costs ~15 HIP calls (~0.15-0.4 ms of API
+// time at 32 MiB slots: H2D, the records call's kernels, D2H, the event);
+// on the caller's thread that time sat between the byte copies of
+// consecutive slots.  Jobs run in flush order, so stream order and the key
+// upload order are the caller's.
+struct Pipeline::Launcher {
+  std::mutex mu;
+  std::condition_variable cv, issued;
+  std::deque<LaunchJob> q;
+  bool stop = false;
+  std::exception_ptr err;  // first enqueue failure; the Pipeline is unusable after it
+  std::thread th;
+};
+
 Pipeline::Pipeline(Direction d, const Options &o) : dir_(d), opt_(o) {
+  hip_check(hipGetDevice(&dev_), "current device");
   if (opt_.depth < 2 || opt_.slot_records == 0 || opt_.slot_bytes < 65536)
     throw std::invalid_argument("pipeline: depth >= 2, slot_records >= 1, slot_bytes >= 64 KiB");
   o_in_ = align256(opt_.slot_records * sizeof(noise_gpu_record));
@@ -258,9 +283,54 @@ Pipeline::Pipeline(Direction d, const Options &o) : dir_(d), opt_(o) {
   hipEvent_t ke = nullptr;
   hip_check(hipEventCreateWithFlags(&ke, hipEventDisableTiming), "key event");
   keys_evt_ = ke;
+  if (opt_.launch_thread) {
+    launcher_ = std::make_unique<Launcher>();
+    Launcher *L = launcher_.get();
+    L->th = std::thread([this, L] {
+      const hipError_t de = hipSetDevice(dev_);
+      std::unique_lock<std::mutex> lk(L->mu);
+      for (;;) {
+        L->cv.wait(lk, [L] { return L->stop || !L->q.empty(); });
+        if (L->q.empty()) return;  // stop, queue drained
+        const LaunchJob j = L->q.front();
+        L->q.pop_front();
+        lk.unlock();
+        std::exception_ptr e;
+        try {
+          if (!L->err) {  // after a failure nothing more is issued
+            hip_check(de, "launcher device");
+            enqueue(j);
+          }
+        } catch (...) {
+          e = std::current_exception();
+        }
+        lk.lock();
+        if (e && !L->err) L->err = e;
+        j.sl->enqueued = true;
+        L->issued.notify_all();
+      }
+    });
+  }
+}
+
+void Pipeline::wait_enqueued(Slot &sl) {
+  if (!launcher_) return;
+  Launcher &L = *launcher_;
+  std::unique_lock<std::mutex> lk(L.mu);
+  L.issued.wait(lk, [&] { return sl.enqueued; });
+  if (L.err) std::rethrow_exception(L.err);
 }
 
 Pipeline::~Pipeline() {
+  if (launcher_) {  // issue what was flushed, then stop
+    {
+      std::lock_guard<std::mutex> lk(launcher_->mu);
+      launcher_->stop = true;
+    }
+    launcher_->cv.notify_all();
+    launcher_->th.join();
+    launcher_->err = nullptr;  // sync_all below waits for whatever was issued
+  }
   try {
     sync_all();
   } catch (...) {
@@ -275,6 +345,14 @@ Pipeline::~Pipeline() {
     (void)hipDeviceSynchronize();
     (void)hipFree(d_keys_);
   }
+  // the records scratch and companion stream cached for each slot stream go
+  // with it (on the Pipeline's device)
+  int cur = dev_;
+  (void)hipGetDevice(&cur);
+  if (cur != dev_) (void)hipSetDevice(dev_);
+  for (Slot *sl : slots_)
+    if (sl->st) (void)noise_gpu_scratch_release(sl->st);
+  if (cur != dev_) (void)hipSetDevice(cur);
   for (Slot *sl : slots_) {
     if (sl->h) (void)hipHostFree(sl->h);
     if (sl->d) (void)hipFree(sl->d);
@@ -287,7 +365,10 @@ Pipeline::~Pipeline() {
 
 void Pipeline::sync_all() {
   for (Slot *sl : slots_)
-    if (sl->in_flight) hip_check(hipEventSynchronize(sl->done), "slot wait");
+    if (sl->in_flight) {
+      wait_enqueued(*sl);
+      hip_check(hipEventSynchronize(sl->done), "slot wait");
+    }
 }
 
 void Pipeline::grow_keys() {
@@ -538,20 +619,49 @@ void Pipeline::copy_out(const Batch &b, std::uint8_t *const *dst) {
 std::uint64_t Pipeline::flush() {
   Slot &sl = *slots_[fill_];
   if (sl.nrec == 0) return 0;
+  const LaunchJob j{&sl, key_dirty_, nonces_.size()};
+  key_dirty_ = j.nkeys;
+  if (launcher_) {
+    {
+      std::lock_guard<std::mutex> lk(launcher_->mu);
+      if (launcher_->err) std::rethrow_exception(launcher_->err);
+      sl.enqueued = false;
+      launcher_->q.push_back(j);
+    }
+    launcher_->cv.notify_one();
+  } else {
+    enqueue(j);
+  }
+  sl.in_flight = true;
+  sl.ticket = ++tickets_;
+  // move on; a slot still in flight is waited for here (back-pressure), and
+  // its results are gone once refilled
+  fill_ = (fill_ + 1) % slots_.size();
+  Slot &nx = *slots_[fill_];
+  if (nx.in_flight) {
+    wait_enqueued(nx);
+    hip_check(hipEventSynchronize(nx.done), "slot wait");
+    nx.in_flight = false;
+  }
+  nx.nrec = nx.in_used = nx.out_used = 0;
+  nx.ticket = 0;
+  return sl.ticket;
+}
+
+void Pipeline::enqueue(const LaunchJob &j) {
+  Slot &sl = *j.sl;
   const bool dec = dir_ == Direction::Decrypt;
-  const std::size_t nkeys = nonces_.size();
   // Key rows reach the device table on the stream of the slot that first
   // needs them.  Every slot stream waits on keys_evt_ before its kernels, and
   // each upload waits on the previous one before recording keys_evt_ again,
   // so the event's latest record covers every row uploaded so far, whichever
   // slot stream carried it.
   if (keys_uploaded_) hip_check(hipStreamWaitEvent(sl.st, static_cast<hipEvent_t>(keys_evt_), 0), "key wait");
-  if (key_dirty_ < nkeys) {  // new sessions' keys (rows never change once written)
-    hip_check(hipMemcpyAsync(d_keys_ + 32 * key_dirty_, h_keys_ + 32 * key_dirty_,
-                             32 * (nkeys - key_dirty_), hipMemcpyHostToDevice, sl.st), "key upload");
+  if (j.key_lo < j.nkeys) {  // new sessions' keys (rows never change once written)
+    hip_check(hipMemcpyAsync(d_keys_ + 32 * j.key_lo, h_keys_ + 32 * j.key_lo, 32 * (j.nkeys - j.key_lo),
+                             hipMemcpyHostToDevice, sl.st), "key upload");
     hip_check(hipEventRecord(static_cast<hipEvent_t>(keys_evt_), sl.st), "key event");
     keys_uploaded_ = true;
-    key_dirty_ = nkeys;
   }
   hip_check(hipMemcpyAsync(sl.d, sl.h, sl.nrec * sizeof(noise_gpu_record), hipMemcpyHostToDevice, sl.st),
             "records H2D");
@@ -559,9 +669,9 @@ std::uint64_t Pipeline::flush() {
     hip_check(hipMemcpyAsync(sl.d + o_in_, sl.h + o_in_, sl.in_used, hipMemcpyHostToDevice, sl.st),
               "messages H2D");
   const auto *d_recs = reinterpret_cast<const noise_gpu_record *>(sl.d);
-  const int rc = dec ? noise_gpu_decrypt_records(d_keys_, (std::uint32_t)nkeys, d_recs, sl.nrec, sl.d + o_in_,
+  const int rc = dec ? noise_gpu_decrypt_records(d_keys_, (std::uint32_t)j.nkeys, d_recs, sl.nrec, sl.d + o_in_,
                                                  sl.d + o_out_, nullptr, sl.d + o_st_, sl.st)
-                     : noise_gpu_encrypt_records(d_keys_, (std::uint32_t)nkeys, d_recs, sl.nrec, sl.d + o_in_,
+                     : noise_gpu_encrypt_records(d_keys_, (std::uint32_t)j.nkeys, d_recs, sl.nrec, sl.d + o_in_,
                                                  sl.d + o_out_, nullptr, sl.st);
   if (rc != NOISE_GPU_OK)
     throw std::runtime_error(std::string("noise-mi355x: ") + noise_gpu_strerror(rc) + ": " +
@@ -573,19 +683,6 @@ std::uint64_t Pipeline::flush() {
     hip_check(hipMemcpyAsync(sl.h + o_st_, sl.d + o_st_, sl.nrec, hipMemcpyDeviceToHost, sl.st),
               "status D2H");
   hip_check(hipEventRecord(sl.done, sl.st), "slot event");
-  sl.in_flight = true;
-  sl.ticket = ++tickets_;
-  // move on; a slot still in flight is waited for here (back-pressure), and
-  // its results are gone once refilled
-  fill_ = (fill_ + 1) % slots_.size();
-  Slot &nx = *slots_[fill_];
-  if (nx.in_flight) {
-    hip_check(hipEventSynchronize(nx.done), "slot wait");
-    nx.in_flight = false;
-  }
-  nx.nrec = nx.in_used = nx.out_used = 0;
-  nx.ticket = 0;
-  return sl.ticket;
 }
 
 Pipeline::Batch Pipeline::wait(std::uint64_t ticket) {
@@ -594,6 +691,7 @@ Pipeline::Batch Pipeline::wait(std::uint64_t ticket) {
     if (c->ticket == ticket && ticket != 0) sl = c;
   if (!sl) throw std::logic_error("pipeline: ticket unknown or its slot was reused");
   if (sl->in_flight) {
+    wait_enqueued(*sl);
     hip_check(hipEventSynchronize(sl->done), "slot wait");
     sl->in_flight = false;
   }

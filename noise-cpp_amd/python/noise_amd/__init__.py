@@ -140,6 +140,7 @@ def load(path=LIB_PATH):
         "noise_gpu_thread_release": (ctypes.c_int, []),
         "noise_gpu_fill_synthetic": (ctypes.c_int, [u8p, u64, u64, u64, vp]),
         "noise_gpu_scratch_wipe": (ctypes.c_int, [vp]),
+        "noise_gpu_scratch_release": (ctypes.c_int, [vp]),
         "noise_gpu_hs_create": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, u64,
                                                ctypes.POINTER(ctypes.c_void_p)]),
         "noise_gpu_hs_destroy": (ctypes.c_int, [vp]),

@@ -46,6 +46,7 @@ static int run_pipeline(int S, int M, std::uint64_t seed) {
     if (!c && fails++ < 20) std::printf("FAIL %s (%ld)\n", what, i);
   };
   nt::Pipeline::Options o;
+  o.launch_thread = seed % 2 == 0;  // odd seeds: flush() issues the HIP work itself
   o.slot_bytes = 256 << 10;  // small slots: many flushes, full-slot retries
   o.slot_records = 97;
   o.depth = 3;
@@ -172,6 +173,7 @@ static int run_pipeline_batch(int S, int M, std::uint64_t seed, std::size_t slot
     if (!c && fails++ < 20) std::printf("FAIL %s (%ld)\n", what, i);
   };
   nt::Pipeline::Options o;
+  o.launch_thread = seed % 2 == 0;  // odd seeds: flush() issues the HIP work itself
   o.slot_bytes = slot_bytes;
   o.slot_records = slot_records;
   o.depth = 3;
@@ -293,7 +295,8 @@ static int run_keyrace(int S) {
 
 // Host-resident throughput: M messages of len bytes from one source buffer
 // (the "socket reads"), encrypt then decrypt, results checksummed (touched).
-static int run_bench(const std::string &mode, int S, long M, std::size_t len, int threads = 1) {
+static int run_bench(const std::string &mode, int S, long M, std::size_t len, int threads = 1,
+                     int depth = 0, int launch = 1, std::size_t slot_records = 0) {
   std::mt19937_64 rng(7);
   bytes src((std::size_t)M * len);
   for (std::size_t i = 0; i < src.size(); i += 8) {
@@ -315,6 +318,12 @@ static int run_bench(const std::string &mode, int S, long M, std::size_t len, in
   // outside the timed region
   nt::Pipeline::Options popt;
   popt.copy_threads = threads;
+  if (depth > 0) popt.depth = depth;
+  popt.launch_thread = launch != 0;
+  if (slot_records) popt.slot_records = slot_records;
+  // results consumed depth - 2 flushes after their own: the next flush
+  // reuses the slot depth - 1 back, and depth - 2 slots stay in flight
+  const std::size_t keep = (std::size_t)popt.depth - 2;
   nt::Pipeline penc(nt::Pipeline::Direction::Encrypt, popt), pdec(nt::Pipeline::Direction::Decrypt, popt);
   for (int s = 0; s < S; ++s) {
     penc.add_session(cs[s]);
@@ -344,7 +353,7 @@ static int run_bench(const std::string &mode, int S, long M, std::size_t len, in
         std::deque<std::pair<std::uint64_t, long>> q;
         std::vector<nt::Pipeline::Message> msgs(M);
         for (long i = 0; i < M; ++i) msgs[i] = {(std::size_t)(i % S), in + i * ilen, ilen};
-        std::vector<std::uint8_t *> dst(1 << 16);
+        std::vector<std::uint8_t *> dst(popt.slot_records);
         auto take = [&](std::size_t keep) {
           while (q.size() > keep) {
             auto [t, f] = q.front();
@@ -374,7 +383,7 @@ static int run_bench(const std::string &mode, int S, long M, std::size_t len, in
             q.push_back({p.flush(), first});
             phase[d][1] += std::chrono::duration<double>(clk::now() - s1).count();
             first = i;
-            take(1);
+            take(keep);
           }
         }
         q.push_back({p.flush(), first});
@@ -402,7 +411,7 @@ static int run_bench(const std::string &mode, int S, long M, std::size_t len, in
           }
           q.push_back({p.flush(), first});
           first = i;
-          take(1);  // depth 3: the next flush reuses the slot two back
+          take(keep);
         }
         q.push_back({p.flush(), first});
         take(0);
@@ -416,12 +425,12 @@ static int run_bench(const std::string &mode, int S, long M, std::size_t len, in
     for (long i = 0; i < M; ++i) sum += ctall[(std::size_t)i * (len + 16)] + ptall[(std::size_t)i * len];
   }
   const double gib = (double)M * len * 2 / (1u << 30);  // two timed passes per direction
-  std::printf("{\"mode\": \"%s\", \"copy_threads\": %d, \"sessions\": %d, \"messages\": %ld, "
+  std::printf("{\"mode\": \"%s\", \"copy_threads\": %d, \"depth\": %d, \"launch_thread\": %d, \"slot_records\": %zu, \"sessions\": %d, \"messages\": %ld, "
               "\"len\": %zu, \"encrypt_gib_s\": %.2f, \"decrypt_gib_s\": %.2f, "
               "\"phases_ms\": {\"encrypt\": [%.1f, %.1f, %.1f, %.1f], \"decrypt\": [%.1f, %.1f, %.1f, %.1f], "
               "\"order\": \"submit_batch, flush, wait, copy_out + status check (batched mode; all passes)\"}, "
               "\"checksum\": %llu}\n",
-              mode.c_str(), threads, S, M, len, gib / secs[0], gib / secs[1], phase[0][0] * 1e3,
+              mode.c_str(), threads, popt.depth, (int)popt.launch_thread, popt.slot_records, S, M, len, gib / secs[0], gib / secs[1], phase[0][0] * 1e3,
               phase[0][1] * 1e3, phase[0][2] * 1e3, phase[0][3] * 1e3, phase[1][0] * 1e3, phase[1][1] * 1e3,
               phase[1][2] * 1e3, phase[1][3] * 1e3, (unsigned long long)sum);
   return 0;
@@ -440,7 +449,8 @@ int main(int argc, char **argv) {
   }
   if (argc > 1 && std::string(argv[1]) == "bench")
     return run_bench(argv[2], std::atoi(argv[3]), std::atol(argv[4]), std::strtoul(argv[5], nullptr, 0),
-                     argc > 6 ? std::atoi(argv[6]) : 1);
+                     argc > 6 ? std::atoi(argv[6]) : 1, argc > 7 ? std::atoi(argv[7]) : 0,
+                     argc > 8 ? std::atoi(argv[8]) : 1, argc > 9 ? std::strtoul(argv[9], nullptr, 0) : 0);
   const int S = argc > 1 ? std::atoi(argv[1]) : 100;
   const int M = argc > 2 ? std::atoi(argv[2]) : 1000;
   std::mt19937_64 rng(argc > 3 ? std::strtoull(argv[3], nullptr, 0) : 1);

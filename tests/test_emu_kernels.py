@@ -77,6 +77,30 @@ def test_host_entry_points_emulated_and_wiped():
     assert "emu_api ok" in r.stdout
 
 
+@pytest.mark.parametrize("args", [
+    ["pipeline", "10", "300", "2"],                       # launcher thread, tiny slots
+    ["pipeline", "10", "300", "3"],                       # flush() issues its own work
+    ["pipeline_batch", "20", "600", "4"],                 # copy pool, ragged batches
+    ["pipeline_batch", "30", "9000", "6", "8192", str(2 << 20), "600", "20000"],  # parallel bookkeeping
+    ["keyrace", "4096"],                                  # key rows uploaded on another slot's stream
+])
+def test_transport_pipeline_emulated(args):
+    """noise::transport::Pipeline (host/transport.cpp: copy pool, launcher
+    thread, parallel submit_batch bookkeeping, key-table uploads) over the
+    emulated C ABI, under AddressSanitizer with leak detection: ciphertexts vs
+    the oracle, nonce accounting, tampered records, and every slot stream's
+    records scratch and companion stream released with the Pipeline."""
+    r = subprocess.run(["make", JOBS, "-C", EMU, "GRID_CAP=3u", "transport"], capture_output=True,
+                       text=True, timeout=900)
+    if r.returncode != 0:
+        pytest.fail("emulation build failed:\n" + r.stdout[-2000:] + r.stderr[-4000:])
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1")
+    r = subprocess.run([os.path.join(EMU, "build", "emu_transport"), *args], capture_output=True,
+                       text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]
+    assert "ok (0 failures)" in r.stdout
+
+
 def test_records_segment_overflow_emulated(emu_bin_small_cap):
     # long records past the 300-segment scratch fall back to the generic kernel
     r = _run(emu_bin_small_cap, "cfg4", 700, 7, 0)

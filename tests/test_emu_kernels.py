@@ -81,7 +81,7 @@ def test_host_entry_points_emulated_and_wiped():
     ["pipeline", "10", "300", "2"],                       # launcher thread, tiny slots
     ["pipeline", "10", "300", "3"],                       # flush() issues its own work
     ["pipeline_batch", "20", "600", "4"],                 # copy pool, ragged batches
-    ["pipeline_batch", "30", "9000", "6", "8192", str(2 << 20), "600", "20000"],  # parallel bookkeeping
+    ["pipeline_batch", "30", "5000", "6", "8192", str(1 << 20), "600", "20000"],  # parallel bookkeeping, byte cut
     ["keyrace", "4096"],                                  # key rows uploaded on another slot's stream
 ])
 def test_transport_pipeline_emulated(args):

@@ -434,6 +434,8 @@ def make_workload(cfg, args, rank, world, stream):
         cfgd = {"record_bytes": L, "ct_stride": L + 16, "keys": 1}
         knames = ((tile_symbol(False, L, True, 0),), (tile_symbol(True, L, True, 0),))
         meta = 0
+        oracle = {"kind": "uniform", "R": R, "L": L, "n_base": n_base, "key": KEY, "seed": SEED,
+                  "data_offset": n_base * L, "pt": d_pt, "ct": d_ct, "back": d_back, "status": d_st}
     elif cfg == 3:
         # 65536 sessions x 16 records x 1 KiB, interleaved: record i belongs to
         # session s = i mod S with nonce (s << 32) + i // S; key of session s =
@@ -469,6 +471,19 @@ def make_workload(cfg, args, rank, world, stream):
                 "session_nonces": "(s << 32) + i // 65536 (the rank is in the key, not the nonce)"}
         knames = ((tile_symbol(False, L, True, 1),), (tile_symbol(True, L, True, 1),))
         meta = 12 * R + 32 * S  # 4-B key index + 8-B nonce per record, key table
+
+        def oracle_descs():
+            r = np.arange(R, dtype=np.uint64)
+            enc = np.zeros(R, dtype=noise_amd.record_dtype())
+            enc["in_off"], enc["out_off"] = r * np.uint64(L), r * np.uint64(L + 16)
+            enc["nonce"] = ((r % np.uint64(S)) << np.uint64(32)) + r // np.uint64(S)
+            enc["len"], enc["key_idx"] = L, (r % np.uint64(S)).astype(np.uint32)
+            dec = enc.copy()
+            dec["in_off"], dec["out_off"] = enc["out_off"], enc["in_off"]
+            return enc, dec
+        oracle = {"kind": "records", "n_base": n_base, "keys": d_keys, "descs": oracle_descs,
+                  "seed": SEED, "data_offset": rank * R * L, "pt_bytes": R * L,
+                  "pt": d_pt, "ct": d_ct, "back": d_back, "status": d_st}
     elif cfg == 4:
         R = args.records or (1 << 20)
         lens = zipf_lengths(R)
@@ -523,6 +538,9 @@ def make_workload(cfg, args, rank, world, stream):
                     return False
             return True
         ct_bytes = int((lens + 16).sum())
+        oracle = {"kind": "records", "n_base": n_base, "keys": np.frombuffer(KEY, dtype=np.uint8).copy(),
+                  "descs": lambda: (enc_d, dec_d), "seed": SEED, "data_offset": 0,
+                  "pt_bytes": tot_in, "pt": d_pt, "ct": d_ct, "back": d_back, "status": d_st}
         # the whole records call (classifier, segment / tail / small-class /
         # generic kernels, finalize): every noise_amd kernel of the direction
         return {"R": R, "L": L, "n_base": n_base, "workload": workload, "step": step, "check": check,
@@ -535,7 +553,7 @@ def make_workload(cfg, args, rank, world, stream):
                            ("noise_amd::k_cls_", "noise_amd::k_seg_prep", "noise_amd::k_seg_tail<true",
                             "noise_amd::k_seg_finalize<true", "noise_amd::k_seg_finalize_w<true", "noise_amd::k_seg_fixup",
                             "noise_amd::k_aead_tile<true", "noise_amd::k_aead_records<true")),
-                "call_level": True}
+                "call_level": True, "oracle": oracle}
     else:
         raise SystemExit("unknown config %d" % cfg)
 
@@ -544,7 +562,7 @@ def make_workload(cfg, args, rank, world, stream):
     return {"R": R, "L": L, "n_base": n_base, "workload": workload, "step": step, "check": check,
             "metric": metric, "config": cfgd, "pt_bytes": R * L,
             "enc_bytes": R * (2 * L + 16) + meta, "dec_bytes": R * (2 * L + 17) + meta,
-            "read_bytes": (R * L + meta, R * (L + 16) + meta), "knames": knames}
+            "read_bytes": (R * L + meta, R * (L + 16) + meta), "knames": knames, "oracle": oracle}
 
 
 def host_inclusive(R, L):
@@ -604,6 +622,10 @@ def parse(argv):
     ap.add_argument("--host-inclusive", action="store_true",
                     help="also time the pinned-host H2D->kernel->D2H pipeline (DESIGN.md)")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
+    # test hook (tests/test_gpu_multirank.py): after the timed run, every rank
+    # compares its WHOLE shard with the CPU oracle (tests/fullcheck.py) at its
+    # global nonce base and data offset; off by default, outside the timing
+    ap.add_argument("--check-oracle", action="store_true", help=argparse.SUPPRESS)
     # layout study (config 4): byte alignment of each record's offsets
     ap.add_argument("--rec-align", type=int, default=16, help=argparse.SUPPRESS)
     # test hook: ranks share the visible GPUs (rank r -> device r mod count),
@@ -693,21 +715,31 @@ def main(argv=None):
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    shards = [{"rank": rank, "nonce_lo": wl["n_base"], "nonce_hi": wl["n_base"] + R, "records": R}]
+    mine = {"rank": rank, "nonce_lo": wl["n_base"], "nonce_hi": wl["n_base"] + R, "records": R}
+    # the timed work was correct too
+    if not wl["check"]():
+        raise SystemExit("timed round trip failed on rank %d" % rank)
+    if args.check_oracle and not args.stub:
+        # test infrastructure (tests/fullcheck.py, the oracle): a checker of
+        # this rank's whole shard, run after the timed region
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import fullcheck
+        import oracle_lib
+        res = fullcheck.check_bench_shard(oracle_lib.Oracle(), torch, wl["oracle"])
+        log("rank %d: oracle check of the whole shard passed: %s" % (rank, json.dumps(res)))
+        mine["oracle_check"] = res
+    shards = [mine]
     if dist:
         red_dev = "cuda" if (dev == "cuda" and args.dist_backend == "nccl") else "cpu"
         elapsed, total_rec = reduce_over_ranks(dist, elapsed, R, red_dev)
         gathered = [None] * world
-        dist.all_gather_object(gathered, shards[0])
+        dist.all_gather_object(gathered, mine)
         shards = gathered
     else:
         total_rec = R
     bad = check_shards(shards) if cfg != 3 else None
     if bad:
         raise SystemExit("shard table: " + bad)
-    # the timed work was correct too
-    if not wl["check"]():
-        raise SystemExit("timed round trip failed on rank %d" % rank)
     if evs:
         enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
         dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps

@@ -330,14 +330,42 @@ int noise_gpu_rekey_host(uint8_t h_key[32]);
  * and is stopped by on = 0 (which also frees the request image),
  * noise_gpu_thread_release, thread exit and library unload; on the way out it
  * zeroes its LDS (speculated keystream, key copies).  While it runs it holds
- * one CU and ~105 KB of its LDS, and a device-wide synchronisation
- * (hipDeviceSynchronize) waits for it to idle out.  A request it does not
- * answer within 10 s fails with NOISE_GPU_E_HIP.  Results, hygiene (the
- * request image is zeroed, but for four sequence words, before the done word)
- * and error behaviour are those of the launch path.  NOISE_GPU_RESIDENT_REQ=
- * host puts the request image in host-mapped memory instead (polled over
- * PCIe).  Records with more than 8192 bytes of AD or more than 65535 bytes
- * take the staged path either way. */
+ * one CU and ~105 KB of its LDS.
+ *
+ * Requests.  Each 16-byte chunk is written with ONE aligned 16-byte store
+ * through the BAR (write-combined), after an sfence that orders it behind
+ * the staged bytes.  The engine does not assume such a store lands whole:
+ * chunk 3 carries a check word, a position-weighted sum of every payload word
+ * of the header and inline chunks, and the workgroup takes a request only
+ * when every chunk carries the new sequence number AND the words sum to the
+ * check word -- a chunk seen half-landed (new sequence number, stale
+ * payload) is polled again.  After ~4096 empty polls the polling wave backs
+ * off (s_sleep between polls).
+ *
+ * Other work on the device.  The workgroup runs on a non-blocking stream of
+ * the highest priority, whose hardware queue normal-priority streams never
+ * share (the runtime maps streams onto a few hardware queues per priority, in
+ * order: a stream sharing the instance's queue would wait until it idles
+ * out).  A process that creates more high-priority streams of its own than
+ * the runtime has queues (GPU_MAX_HW_QUEUES, default 4) may share it.  Device
+ * memory the engine frees while running (records scratch that grows, staging,
+ * a Pipeline's key table) is freed stream-ordered, so batch calls and
+ * Pipelines on other threads never wait for the instance.  What still waits
+ * for it to idle out (or for on = 0): hipDeviceSynchronize, hipFree and
+ * hipHostFree (which on ROCm wait for every stream of the device) -- in the
+ * engine: noise_gpu_ctx_destroy, noise_gpu_thread_release / thread exit of
+ * ANOTHER thread, noise_gpu_hs_destroy, and a Pipeline's destructor.
+ *
+ * Stopping.  on = 0 sets the stop word and waits -- at most 10 s -- for the
+ * workgroup's alive word before it synchronises the stream; an instance that
+ * does not leave in that time makes the call fail with NOISE_GPU_E_HIP and
+ * the context unusable (every later call on it fails; nothing it reads is
+ * freed).  A request it does not answer within 10 s fails the same way.
+ * Results, hygiene (the request image is zeroed, but for four sequence words,
+ * before the done word) and error behaviour are those of the launch path.
+ * NOISE_GPU_RESIDENT_REQ=host puts the request image in host-mapped memory
+ * instead (polled over PCIe).  Records with more than 8192 bytes of AD or more
+ * than 65535 bytes take the staged path either way. */
 int noise_gpu_set_resident(int on, uint32_t idle_us);
 
 /* Descriptor batch between HOST buffers (synchronous): the key table

@@ -63,7 +63,7 @@ static_assert(sizeof(OneRing) == 64, "stop line");
 // that the kernel polls:
 //   chunk 0: seq, len | ad_len << 16 | decrypt << 30, nonce lo, nonce hi
 //   chunk 1: seq, key words 0, 1, 2      chunk 2: seq, key words 3, 4, 5
-//   chunk 3: seq, key words 6, 7, 0
+//   chunk 3: seq, key words 6, 7, check word (req_check_word)
 //   chunks 4 ..: a small record INLINE -- its staged image (AD | pad |
 //     record | pad | tag, the 16-byte pieces the kernel works on) 12 bytes
 //     per chunk, so every chunk carries the seq that validates it and the
@@ -83,6 +83,17 @@ __host__ __device__ constexpr bool req_inline(uint32_t ad_len, uint32_t len, boo
 }
 __host__ __device__ constexpr uint32_t req_inline_chunks(uint32_t ad_len, uint32_t len, bool decrypt) {
   return req_inline(ad_len, len, decrypt) ? (req_image_bytes(ad_len, len, decrypt) + 11u) / 12u : 0u;
+}
+// The request's check word (chunk 3, word 3): a position-weighted 32-bit sum
+// of the three payload words of every header chunk (chunk 3 counts with its
+// check word as 0) and every inline chunk.  The kernel takes a request only
+// when all its chunks carry the new seq AND their words sum to the check
+// word, so a chunk whose 16-byte BAR store has landed in part (new seq,
+// stale payload) is polled again instead of served.
+constexpr uint32_t kReqCheckSalt = 0x9e3779b9u;
+__host__ __device__ constexpr uint32_t req_check_mix(uint32_t chunk, uint32_t w1, uint32_t w2,
+                                                     uint32_t w3) {
+  return w1 * (6u * chunk + 1u) + w2 * (6u * chunk + 3u) + w3 * (6u * chunk + 5u);
 }
 __host__ __device__ constexpr OneLayout one_layout(uint32_t ad_len, uint32_t len) {
   const uint64_t a16 = (ad_len + 15ull) & ~15ull, l16 = (len + 15ull) & ~15ull;

@@ -18,6 +18,7 @@
 #include <string>
 
 #include "launchers.hpp"
+#include "noise_amd/dev_mem.hpp"
 #include "noise_gpu.h"
 
 namespace {
@@ -110,9 +111,9 @@ struct Staging {
     int cur = -1;
     if (stream && dev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != dev) (void)hipSetDevice(dev);
     if (stream) (void)noise_amd::records_scratch_release(stream);
-    if (d) {
-      (void)hipMemset(d, 0, cap);
-      (void)hipFree(d);
+    if (d) {  // wiped and freed stream-ordered (dev_mem.hpp), then waited for
+      (void)noise_amd::dev_wipe_free(d, cap, stream);
+      (void)hipStreamSynchronize(stream);
     }
     if (h) {
       std::memset(h, 0, cap);
@@ -143,10 +144,16 @@ struct Staging {
     if (bytes <= cap) return NOISE_GPU_OK;
     size_t want = cap ? cap : 4096;
     while (want < bytes) want *= 2;
-    if (d) (void)hipFree(d);
-    if (h) (void)hipHostFree(h);
+    // grow: the old device buffer is wiped and freed after this stream's
+    // earlier work (a hipFree would wait for every stream of the device)
+    if (d) (void)noise_amd::dev_wipe_free(d, cap, stream);
+    if (h) {
+      (void)hipStreamSynchronize(stream);  // its copies are done with it
+      std::memset(h, 0, cap);
+      (void)hipHostFree(h);
+    }
     d = nullptr; h = nullptr; cap = 0;
-    HIP_TRY(hipMalloc(&d, want));
+    HIP_TRY(noise_amd::dev_alloc(reinterpret_cast<void **>(&d), want, stream));
     HIP_TRY(hipHostMalloc(&h, want, hipHostMallocDefault));
     cap = want;
     return NOISE_GPU_OK;
@@ -225,21 +232,53 @@ struct OneCtx {
   // resident request image (OneReq, launchers.hpp): host and device views
   uint8_t *hreq = nullptr, *dreq = nullptr;
   int req_kind = kReqFine;
-  // the launch path's stream while in resident mode (the resident instance
-  // occupies `stream`): records the resident kernel does not serve
-  hipStream_t lstream_res = nullptr;
-  hipStream_t lstream = nullptr;
+  // The resident instance's stream, on a hardware queue of its own.  The HIP
+  // runtime maps a process's streams onto GPU_MAX_HW_QUEUES (4 by default)
+  // hardware queues per priority level, and a queue runs its packets in
+  // order: a stream sharing the instance's queue -- another thread's batch
+  // work, a Pipeline slot -- would wait until the instance idles out (seen on
+  // MI355X: a Pipeline slot stuck for the whole resident run).  So the
+  // instance runs on a non-blocking stream of the HIGHEST priority, whose
+  // queue pool is separate from the normal-priority streams'; it shares a
+  // queue only if the process creates more high-priority streams than that
+  // pool has queues.  (A CU-masked stream also gets a queue of its own, but
+  // it is a blocking stream: every null-stream operation -- hipMemcpy, the
+  // stream-ordered allocator -- then waits for the instance.)  `stream` stays
+  // the launch path's.
+  hipStream_t rstream = nullptr;
   ~OneCtx() { release(); }
   noise_amd::OneRing *ring() { return reinterpret_cast<noise_amd::OneRing *>(h + noise_amd::kOneRingOff); }
-  // stop word -> the instance leaves at its next poll; wait for it
-  void stop_resident() {
-    if (!launched) return;
+  // the instance did not leave on the stop word within kOneWaitLimit: its
+  // stream is never synchronised again (that wait would not end) and every
+  // later call on this context fails with NOISE_GPU_E_HIP
+  bool wedged = false;
+  // stop word -> the instance leaves at its next poll (every 32 polls, a few
+  // microseconds); wait for its alive word, bounded, before the stream sync
+  int stop_resident() {
+    if (wedged) {
+      g_last_error = "resident latency kernel did not stop (context unusable)";
+      return NOISE_GPU_E_HIP;
+    }
+    if (!launched) return NOISE_GPU_OK;
     volatile uint32_t *stop = &ring()->stop;
     *stop = 1u;
-    if (stream) (void)hipStreamSynchronize(stream);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 1; *alive() != 0u; ++spin) {
+      // an instance that never ran (or faulted) does not clear the word:
+      // a stream that has ended or failed needs no more waiting
+      if ((spin & 4095u) == 0u && rstream && hipStreamQuery(rstream) != hipErrorNotReady) break;
+      if (std::chrono::steady_clock::now() - t0 > kOneWaitLimit) {
+        wedged = true;  // the stop word stays set
+        g_last_error = "resident latency kernel did not stop within 10 s (context unusable)";
+        return NOISE_GPU_E_HIP;
+      }
+      _mm_pause();
+    }
+    if (rstream) (void)hipStreamSynchronize(rstream);
     *stop = 0u;
     launched = false;
     resident_track(this, false);
+    return NOISE_GPU_OK;
   }
   void release_req() {
     if (!hreq) return;
@@ -273,13 +312,18 @@ struct OneCtx {
   void release() {
     int cur = -1;
     if (stream && dev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != dev) (void)hipSetDevice(dev);
-    stop_resident();
+    if (stop_resident() != NOISE_GPU_OK) {
+      // a wedged instance still runs from this context's memory: leave it all
+      // allocated (leaked) rather than free it under the kernel or hang here
+      if (cur >= 0 && cur != dev) (void)hipSetDevice(cur);
+      return;
+    }
     if (stream) (void)hipStreamSynchronize(stream);
     release_req();
-    if (lstream_res) {
-      (void)hipStreamSynchronize(lstream_res);
-      (void)hipStreamDestroy(lstream_res);
-      lstream_res = nullptr;
+    if (rstream) {
+      (void)hipStreamSynchronize(rstream);
+      (void)hipStreamDestroy(rstream);
+      rstream = nullptr;
     }
     if (h) {
       std::memset(h, 0, cap);
@@ -301,8 +345,10 @@ struct OneCtx {
       dev = cur;
       HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     }
+    if (wedged) return stop_resident();
     if (bytes <= cap) return NOISE_GPU_OK;
-    stop_resident();  // a running instance holds the old image's address
+    // a running instance holds the old image's address
+    if (int rc = stop_resident()) return rc;
     size_t want = cap ? cap : 16384;
     while (want < bytes) want *= 2;
     if (h) {
@@ -320,9 +366,17 @@ struct OneCtx {
     return NOISE_GPU_OK;
   }
   volatile uint32_t *alive() { return reinterpret_cast<volatile uint32_t *>(h + kOneAliveOff); }
+  int make_rstream() {
+    if (rstream) return NOISE_GPU_OK;
+    int least = 0, greatest = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIP_TRY(hipStreamCreateWithPriority(&rstream, hipStreamNonBlocking, greatest));
+    return NOISE_GPU_OK;
+  }
   int launch_resident(uint32_t last) {
+    if (int rc = make_rstream()) return rc;
     *alive() = 1u;  // the instance clears it when it leaves
-    const hipError_t e = noise_amd::launch_aead_resident(dreq, d, last, idle_us, stream);
+    const hipError_t e = noise_amd::launch_aead_resident(dreq, d, last, idle_us, rstream);
     if (e != hipSuccess) return hip_fail(e, "launch_aead_resident");
     if (!launched) resident_track(this, true);
     launched = true;
@@ -333,21 +387,30 @@ struct OneCtx {
   // kernel cannot see the request (or is wedged): stop it and fail the call
   // rather than spin for ever.
   // by_resident: the request went to the resident instance (else a launch on
-  // lstream, the launch path's stream)
+  // `stream`, the launch path's)
   int wait(uint32_t s, bool by_resident) {
-    hipStream_t wst = by_resident ? stream : lstream;
+    hipStream_t wst = by_resident ? rstream : stream;
     volatile uint32_t *done = reinterpret_cast<volatile uint32_t *>(h);
     const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t spin = 0;; ++spin) {
       if (*done == s) return NOISE_GPU_OK;
+      // the instance left on its idle timer after its last poll (it clears
+      // the alive word last, after any done word it wrote): relaunch now
+      // instead of after the first stream query below
+      if (by_resident && (spin & 63u) == 63u && *alive() == 0u) {
+        if (*done == s) return NOISE_GPU_OK;
+        const int rc = launch_resident(s - 1u);
+        if (rc) return rc;
+        continue;
+      }
       if ((spin & 1023u) == 1023u) {  // now and then: has the stream failed or ended?
         const auto waited = std::chrono::steady_clock::now() - t0;
         // a record takes microseconds: the stream query (a runtime call of
         // ~1 us) is for the rare stall, not for every call's last spins
         if (waited < std::chrono::microseconds(100)) continue;
         if (waited > kOneWaitLimit) {
-          if (by_resident) stop_resident();
-          g_last_error = "latency kernel gave no answer within 10 s";
+          if (by_resident) (void)stop_resident();  // bounded; marks the context wedged
+          if (!wedged) g_last_error = "latency kernel gave no answer within 10 s";
           return NOISE_GPU_E_HIP;
         }
         const hipError_t e = hipStreamQuery(wst);
@@ -414,16 +477,12 @@ int one_record(bool dec, const uint8_t key[32], uint64_t nonce, const uint8_t *a
   if (rc) return rc;
   if (c.resident && (rc = c.reserve_req())) return rc;
   // the resident kernel serves records of <= 63 keystream blocks; a bigger
-  // one is a launch (a second stream: the resident instance holds the first)
+  // one is a launch on the launch path's stream (the instance has its own)
   const bool res = c.resident && len <= noise_amd::kResidentMaxLen;
-  c.lstream = c.stream;
-  if (c.resident && !res) {
-    if (!c.lstream_res) HIP_TRY(hipStreamCreateWithFlags(&c.lstream_res, hipStreamNonBlocking));
-    c.lstream = c.lstream_res;
-  }
   uint32_t s = ++c.seq;
   if (s == 0) s = c.seq = 1;
   const uint32_t n_inl = res ? noise_amd::req_inline_chunks(ad_len, len, dec) : 0u;
+  uint32_t chk = noise_amd::kReqCheckSalt;  // the request's check word (launchers.hpp)
   if (n_inl) {
     // a small record goes inline: its staged image (AD | pad | record | pad
     // | tag) 12 bytes per 16-byte chunk {seq, 3 words} (launchers.hpp OneReq)
@@ -437,7 +496,9 @@ int one_record(bool dec, const uint8_t key[32], uint64_t nonce, const uint8_t *a
     for (uint32_t i = 0; i < n_inl; ++i) {
       uint32_t w[3];
       std::memcpy(w, im + 12u * i, 12);
+      chk += noise_amd::req_check_mix(4u + i, w[0], w[1], w[2]);
       _mm_store_si128(q + i, _mm_setr_epi32((int)s, (int)w[0], (int)w[1], (int)w[2]));
+      w[0] = w[1] = w[2] = 0u;
     }
     explicit_bzero(im, 12u * n_inl);  // the plaintext copy on the stack goes too
   } else {
@@ -457,16 +518,22 @@ int one_record(bool dec, const uint8_t key[32], uint64_t nonce, const uint8_t *a
     // takes the request once all four (and any inline chunks) carry seq
     _mm_sfence();
     const uint32_t meta = len | (ad_len << 16) | ((uint32_t)dec << 30);
+    const uint32_t nlo = (uint32_t)nonce, nhi = (uint32_t)(nonce >> 32);
+    chk += noise_amd::req_check_mix(0u, meta, nlo, nhi) + noise_amd::req_check_mix(1u, k[0], k[1], k[2]) +
+           noise_amd::req_check_mix(2u, k[3], k[4], k[5]) + noise_amd::req_check_mix(3u, k[6], k[7], 0u);
     __m128i *q = reinterpret_cast<__m128i *>(c.hreq);
     _mm_store_si128(q + 1, _mm_setr_epi32((int)s, (int)k[0], (int)k[1], (int)k[2]));
     _mm_store_si128(q + 2, _mm_setr_epi32((int)s, (int)k[3], (int)k[4], (int)k[5]));
-    _mm_store_si128(q + 3, _mm_setr_epi32((int)s, (int)k[6], (int)k[7], 0));
-    _mm_store_si128(q + 0, _mm_setr_epi32((int)s, (int)meta, (int)(uint32_t)nonce,
-                                          (int)(uint32_t)(nonce >> 32)));
+    _mm_store_si128(q + 3, _mm_setr_epi32((int)s, (int)k[6], (int)k[7], (int)chk));
+    _mm_store_si128(q + 0, _mm_setr_epi32((int)s, (int)meta, (int)nlo, (int)nhi));
     _mm_sfence();
-    if (!c.launched) rc = c.launch_resident(s - 1u);
+    chk = 0u;
+    // (re)launch when no instance runs: never launched, or the last one left
+    // on its idle timer (it clears the alive word on its way out, after its
+    // last poll -- a request rung after that poll is this one's to serve)
+    if (!c.launched || *c.alive() == 0u) rc = c.launch_resident(s - 1u);
   } else {
-    const hipError_t e = noise_amd::launch_aead_one(dec, k, nonce, c.d, len, ad_len, s, c.lstream);
+    const hipError_t e = noise_amd::launch_aead_one(dec, k, nonce, c.d, len, ad_len, s, c.stream);
     if (e != hipSuccess) rc = hip_fail(e, "launch_aead_one");
   }
   std::memset(k, 0, sizeof k);
@@ -487,8 +554,7 @@ int one_record(bool dec, const uint8_t key[32], uint64_t nonce, const uint8_t *a
   std::memset(c.h + 4, 0, 4);
   if (res) {
     std::memset(c.h + lay.out, 0, lay.total - lay.out);
-    if (rc != NOISE_GPU_OK && c.hreq) {
-      c.stop_resident();
+    if (rc != NOISE_GPU_OK && c.hreq && c.stop_resident() == NOISE_GPU_OK) {
       if (c.req_kind == kReqHost) std::memset(c.hreq, 0, noise_amd::kOneReqBytes);
       else (void)hipMemset(c.dreq, 0, noise_amd::kOneReqBytes);
     }
@@ -890,11 +956,8 @@ struct PipeCtx {
   ~PipeCtx() { release(); }
   void release() {
     for (int i = 0; i < kDepth; ++i) {
+      if (buf[i]) (void)noise_amd::dev_wipe_free(buf[i], kChunk + (kChunk >> 4), st[i]);
       if (st[i]) (void)hipStreamSynchronize(st[i]);
-      if (buf[i]) {
-        (void)hipMemset(buf[i], 0, kChunk + (kChunk >> 4));
-        (void)hipFree(buf[i]);
-      }
       if (st[i]) (void)hipStreamDestroy(st[i]);
       buf[i] = nullptr;
       st[i] = nullptr;
@@ -908,7 +971,7 @@ struct PipeCtx {
     release();
     for (int i = 0; i < kDepth; ++i) {
       HIP_TRY(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
-      HIP_TRY(hipMalloc(&buf[i], kChunk + (kChunk >> 4)));
+      HIP_TRY(noise_amd::dev_alloc(reinterpret_cast<void **>(&buf[i]), kChunk + (kChunk >> 4), st[i]));
     }
     dev = cur;
     return NOISE_GPU_OK;
@@ -1060,14 +1123,12 @@ static int set_resident(OneCtx &c, int on, uint32_t idle_us) {
     int rc = check_device();
     if (rc) return rc;
     c.idle_us = idle_us ? idle_us : kResidentIdleDefaultUs;
-    if (c.resident) {  // new idle time: the next instance takes it
-      c.stop_resident();
-      return NOISE_GPU_OK;
-    }
+    if (c.resident)  // new idle time: the next instance takes it
+      return c.stop_resident();
     c.resident = true;
     return NOISE_GPU_OK;
   }
-  c.stop_resident();
+  if (int rc = c.stop_resident()) return rc;  // wedged: the image stays (the kernel reads it)
   c.release_req();  // zeroed and freed: nothing of the mode stays behind
   c.resident = false;
   return NOISE_GPU_OK;

@@ -32,6 +32,7 @@
 
 #include "chachapoly_device.hpp"
 #include "launchers.hpp"
+#include "noise_amd/dev_mem.hpp"
 #include "tile_kernel.hpp"
 
 namespace noise_amd {
@@ -784,9 +785,11 @@ __global__ __launch_bounds__(kGenBlock) void k_aead_records(
 }
 
 // ---- scratch: one grow-only buffer per (device, stream) ------------------
-// Calls on one stream are ordered, so they may share the buffer; a buffer
-// only grows (hipFree waits for the device, so a smaller one still in use by
-// an earlier launch is never released under it).
+// Calls on one stream are ordered, so they may share the buffer.  It only
+// grows; the smaller one is wiped and freed stream-ordered (dev_mem.hpp), so
+// it is released after the launches that still use it, and the grow waits for
+// nothing else on the device (hipFree would wait for every stream, e.g. for a
+// resident latency instance serving another thread).
 struct ScratchEntry {
   int dev;
   hipStream_t stream;
@@ -817,17 +820,17 @@ static hipError_t scratch_get(void **p, size_t bytes, hipStream_t stream) {
   for (Entry &en : cache) {
     if (en.dev != dev || en.stream != stream) continue;
     if (en.size < bytes) {
-      if ((e = hipFree(en.ptr)) != hipSuccess) return e;
+      if ((e = dev_wipe_free(en.ptr, en.size, stream)) != hipSuccess) return e;
       en.ptr = nullptr;
       en.size = 0;
-      if ((e = hipMalloc(&en.ptr, bytes)) != hipSuccess) return e;
+      if ((e = dev_alloc(&en.ptr, bytes, stream)) != hipSuccess) return e;
       en.size = bytes;
     }
     *p = en.ptr;
     return hipSuccess;
   }
   void *ptr = nullptr;
-  if ((e = hipMalloc(&ptr, bytes)) != hipSuccess) return e;
+  if ((e = dev_alloc(&ptr, bytes, stream)) != hipSuccess) return e;
   cache.push_back({dev, stream, ptr, bytes});
   *p = ptr;
   return hipSuccess;
@@ -857,7 +860,6 @@ hipError_t records_scratch_release(hipStream_t stream) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
-  e = hipStreamSynchronize(stream);
   void *ptr = nullptr;
   size_t size = 0;
   {
@@ -870,12 +872,9 @@ hipError_t records_scratch_release(hipStream_t stream) {
         break;
       }
   }
-  if (ptr) {
-    hipError_t e2 = hipMemset(ptr, 0, size);
-    if (e == hipSuccess) e = e2;
-    e2 = hipFree(ptr);
-    if (e == hipSuccess) e = e2;
-  }
+  if (ptr) e = dev_wipe_free(ptr, size, stream);  // after the calls queued on `stream`
+  const hipError_t e2 = hipStreamSynchronize(stream);
+  if (e == hipSuccess) e = e2;
   const hipError_t e3 = aux_release(dev, stream);
   return e == hipSuccess ? e3 : e;
 }

@@ -851,10 +851,27 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_resident(uint8_t *req, uint8
           n_inl = req_inline_chunks((meta >> 16) & 0x3fffu, meta & 0xffffu, (meta >> 30) & 1u);
           const bool need0 = lane >= 4u && lane - 4u < n_inl, need1 = 60u + lane < n_inl;
           if (__ballot((need0 && c.x != seq) || (need1 && c1.x != seq)) == 0ull) {
-            NOISE_ONE_STAMP(0);
-            break;
+            // every chunk carries seq; the words must also sum to the check
+            // word (launchers.hpp req_check_mix), else a chunk landed in part
+            uint32_t v = 0u;
+            if (lane < 4u || need0) v = req_check_mix(lane, c.y, c.z, lane == 3u ? 0u : c.w);
+            if (need1) v += req_check_mix(64u + lane, c1.y, c1.z, c1.w);
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) v += (uint32_t)__shfl_xor((int)v, d);
+            if (v + kReqCheckSalt == (uint32_t)__shfl((int)c.w, 3)) {
+              NOISE_ONE_STAMP(0);
+              break;
+            }
           }
         }
+#ifndef NOISE_RES_SLEEP_POLLS  // empty polls before the wave starts to s_sleep between polls
+#define NOISE_RES_SLEEP_POLLS 4096u
+#endif
+        // a long-idle instance backs off (s_sleep 32: ~2048 clocks, about one
+        // more poll round trip, between polls): half the poll traffic and
+        // issue slots; a request that follows the previous one within a few
+        // ms is still seen at the full poll rate
+        if (polls >= NOISE_RES_SLEEP_POLLS) __builtin_amdgcn_s_sleep(32);
         if ((++polls & 31u) == 0u &&
             (__hip_atomic_load(&ring->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
              __builtin_amdgcn_s_memrealtime() - t_last > idle_ticks)) {

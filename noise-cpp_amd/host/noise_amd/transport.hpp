@@ -183,6 +183,7 @@ class Pipeline {
   std::vector<std::uint64_t> nonces_;
   std::uint8_t *h_keys_ = nullptr, *d_keys_ = nullptr;  // pinned mirror / device table
   std::size_t key_cap_ = 0, key_dirty_ = 0;
+  std::vector<std::uint8_t *> retired_h_;  // outgrown pinned key mirrors (wiped)
   void *keys_evt_ = nullptr;  // hipEvent_t: latest key-row upload (any slot stream)
   bool keys_uploaded_ = false;
   struct CopyPool;

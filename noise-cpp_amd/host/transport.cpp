@@ -15,9 +15,13 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include "noise_amd/dev_mem.hpp"
 #include "noise_gpu.h"
 
 namespace noise::transport {
+
+using noise_amd::dev_alloc;
+using noise_amd::dev_wipe_free;
 
 void append_frame(std::vector<std::uint8_t> &stream, const std::uint8_t *msg, std::size_t len) {
   if (len > kMaxMessage) throw std::length_error("Noise message exceeds 65535 bytes");
@@ -180,8 +184,15 @@ struct Pipeline::CopyPool {
   }
   // fn(lo, hi) over [0, n) in nthr contiguous chunks
   void run(std::size_t n, const std::function<void(std::size_t, std::size_t)> &fn) {
+    run_idx(n, [&fn](std::size_t, std::size_t lo, std::size_t hi) { fn(lo, hi); });
+  }
+  // fn(c, lo, hi): chunk c of [0, n) is [n c / nthr, n (c + 1) / nthr) --
+  // or, below 64 items or with one thread, chunk 0 is all of [0, n) and the
+  // others do not run.  The caller is given c, so a chunk's index never has
+  // to be re-derived from lo (empty chunks when n < nthr share their lo).
+  void run_idx(std::size_t n, const std::function<void(std::size_t, std::size_t, std::size_t)> &fn) {
     if (nthr == 1 || n < 64) {
-      fn(0, n);
+      fn(0, 0, n);
       return;
     }
     {
@@ -192,7 +203,7 @@ struct Pipeline::CopyPool {
       ++gen;
     }
     cv.notify_all();
-    fn(0, n / nthr);
+    fn(0, 0, n / nthr);
     std::unique_lock<std::mutex> lk(mu);
     done.wait(lk, [this] { return pending == 0; });
     job = nullptr;
@@ -200,7 +211,7 @@ struct Pipeline::CopyPool {
   void worker(int w) {
     std::uint64_t seen = 0;
     for (;;) {
-      const std::function<void(std::size_t, std::size_t)> *fn;
+      const std::function<void(std::size_t, std::size_t, std::size_t)> *fn;
       std::size_t n;
       {
         std::unique_lock<std::mutex> lk(mu);
@@ -210,7 +221,7 @@ struct Pipeline::CopyPool {
         fn = job;
         n = total;
       }
-      (*fn)(n * w / nthr, n * (w + 1) / nthr);
+      (*fn)((std::size_t)w, n * w / nthr, n * (w + 1) / nthr);
       {
         std::lock_guard<std::mutex> lk(mu);
         if (--pending == 0) done.notify_one();
@@ -221,7 +232,7 @@ struct Pipeline::CopyPool {
   std::vector<std::thread> th;
   std::mutex mu;
   std::condition_variable cv, done;
-  const std::function<void(std::size_t, std::size_t)> *job = nullptr;
+  const std::function<void(std::size_t, std::size_t, std::size_t)> *job = nullptr;
   std::size_t total = 0;
   std::uint64_t gen = 0;
   int pending = 0;
@@ -275,8 +286,9 @@ Pipeline::Pipeline(Direction d, const Options &o) : dir_(d), opt_(o) {
     slots_.push_back(sl);
     hip_check(hipHostMalloc(reinterpret_cast<void **>(&sl->h), slot_total_, hipHostMallocDefault),
               "pinned slot");
-    hip_check(hipMalloc(reinterpret_cast<void **>(&sl->d), slot_total_), "device slot");
     hip_check(hipStreamCreateWithFlags(&sl->st, hipStreamNonBlocking), "slot stream");
+    hip_check(dev_alloc(reinterpret_cast<void **>(&sl->d), slot_total_, sl->st), "device slot");
+    hip_check(hipStreamSynchronize(sl->st), "device slot");
     hip_check(hipEventCreateWithFlags(&sl->done, hipEventDisableTiming), "slot event");
   }
   pool_ = std::make_unique<CopyPool>(opt_.copy_threads);
@@ -340,10 +352,14 @@ Pipeline::~Pipeline() {
     for (std::size_t i = 0; i < 32 * key_cap_; ++i) kv[i] = 0;
     (void)hipHostFree(h_keys_);
   }
+  for (std::uint8_t *p : retired_h_) (void)hipHostFree(p);  // wiped when retired
+  // Device memory is wiped and freed stream-ordered on the slot streams
+  // (dev_mem.hpp), after sync_all: no device-wide wait, so a resident latency
+  // instance serving another thread does not hold this up.  (hipHostFree
+  // below still waits for every stream of the device: noise_gpu.h.)
   if (d_keys_) {
-    (void)hipMemset(d_keys_, 0, 32 * key_cap_);
-    (void)hipDeviceSynchronize();
-    (void)hipFree(d_keys_);
+    (void)dev_wipe_free(d_keys_, 32 * key_cap_, slots_[0]->st);
+    (void)hipStreamSynchronize(slots_[0]->st);
   }
   // the records scratch and companion stream cached for each slot stream go
   // with it (on the Pipeline's device)
@@ -354,8 +370,14 @@ Pipeline::~Pipeline() {
     if (sl->st) (void)noise_gpu_scratch_release(sl->st);
   if (cur != dev_) (void)hipSetDevice(cur);
   for (Slot *sl : slots_) {
-    if (sl->h) (void)hipHostFree(sl->h);
-    if (sl->d) (void)hipFree(sl->d);
+    if (sl->d && sl->st) {  // the messages in and out: wiped, then freed
+      (void)dev_wipe_free(sl->d, slot_total_, sl->st);
+      (void)hipStreamSynchronize(sl->st);
+    }
+    if (sl->h) {
+      std::memset(sl->h, 0, slot_total_);
+      (void)hipHostFree(sl->h);
+    }
     if (sl->st) (void)hipStreamDestroy(sl->st);
     if (sl->done) (void)hipEventDestroy(sl->done);
     delete sl;
@@ -373,20 +395,29 @@ void Pipeline::sync_all() {
 
 void Pipeline::grow_keys() {
   // the device table may be read by slots in flight: let them finish first
+  // (sync_all also waits until the launcher has issued every flushed slot, so
+  // nothing else enqueues on slot 0's stream, which carries the table below)
   sync_all();
   const std::size_t cap = key_cap_ ? 2 * key_cap_ : 1024;
+  hipStream_t ks = slots_[0]->st;
   std::uint8_t *h = nullptr, *d = nullptr;
   hip_check(hipHostMalloc(reinterpret_cast<void **>(&h), 32 * cap, hipHostMallocDefault), "pinned keys");
-  hip_check(hipMalloc(reinterpret_cast<void **>(&d), 32 * cap), "device keys");
+  // stream-ordered (dev_mem.hpp): no device-wide wait here, so a resident
+  // latency instance on another thread cannot hold up add_session()
+  hip_check(dev_alloc(reinterpret_cast<void **>(&d), 32 * cap, ks), "device keys");
   if (key_cap_) {
     std::memcpy(h, h_keys_, 32 * key_cap_);
-    hip_check(hipMemcpy(d, d_keys_, 32 * key_cap_, hipMemcpyDeviceToDevice), "key table copy");
+    hip_check(hipMemcpyAsync(d, d_keys_, 32 * key_cap_, hipMemcpyDeviceToDevice, ks), "key table copy");
+    hip_check(dev_wipe_free(d_keys_, 32 * key_cap_, ks), "old key table");
+  }
+  hip_check(hipStreamSynchronize(ks), "key table");
+  if (key_cap_) {
+    // the old pinned mirror is wiped now and freed with the Pipeline:
+    // hipHostFree waits for every stream of the device (noise_gpu.h), and
+    // the mirrors double, so the retired ones add up to less than the current
     volatile std::uint8_t *kv = h_keys_;
     for (std::size_t i = 0; i < 32 * key_cap_; ++i) kv[i] = 0;
-    (void)hipHostFree(h_keys_);
-    (void)hipMemset(d_keys_, 0, 32 * key_cap_);
-    (void)hipDeviceSynchronize();
-    (void)hipFree(d_keys_);
+    retired_h_.push_back(h_keys_);
   }
   h_keys_ = h;
   d_keys_ = d;
@@ -506,15 +537,12 @@ std::size_t Pipeline::submit_batch(const Message *messages, std::size_t n) {
   auto refused = [&](const Message &m) {
     return m.session >= S || (dec ? (m.len < 16 || m.len > kMaxMessage) : m.len + 16 > kMaxMessage);
   };
-  // the pool's chunk c of [0, len) is [len c / T, len (c + 1) / T) (one
-  // chunk below 64 messages); its index from its first message
-  auto chunk_of = [T](std::size_t lo, std::size_t len) {
-    return len < 64 ? std::size_t(0) : (lo * T + len - 1) / len;
-  };
+  // the pool's chunk c of [0, len) is [len c / T, len (c + 1) / T), or all
+  // of it in chunk 0 below 64 messages (CopyPool::run_idx passes c)
   // 1. per chunk: the first refused message, the input bytes before it
+  //    (n0 >= 4096 here: every chunk is the T-way split the walk below uses)
   std::vector<std::size_t> bad(T, n0), bytes(T, 0);
-  pool_->run(n0, [&](std::size_t lo, std::size_t hi) {
-    const std::size_t c = chunk_of(lo, n0);
+  pool_->run_idx(n0, [&](std::size_t c, std::size_t lo, std::size_t hi) {
     std::size_t b = 0;
     for (std::size_t i = lo; i < hi; ++i) {
       if (refused(messages[i])) {
@@ -551,8 +579,7 @@ std::size_t Pipeline::submit_batch(const Message *messages, std::size_t n) {
   // 2. per chunk of [0, k): its messages per session and its bytes
   sess_cnt_.assign(T * S, 0u);
   std::vector<std::size_t> in_b(T + 1, 0), out_b(T + 1, 0);
-  pool_->run(k, [&](std::size_t lo, std::size_t hi) {
-    const std::size_t c = chunk_of(lo, k);
+  pool_->run_idx(k, [&](std::size_t c, std::size_t lo, std::size_t hi) {
     std::uint32_t *cnt = sess_cnt_.data() + c * S;
     std::size_t bi = 0, bo = 0;
     for (std::size_t i = lo; i < hi; ++i) {
@@ -586,8 +613,7 @@ std::size_t Pipeline::submit_batch(const Message *messages, std::size_t n) {
   }
   // 3. descriptors and copies
   const std::size_t base = sl.nrec;
-  pool_->run(k, [&](std::size_t lo, std::size_t hi) {
-    const std::size_t c = chunk_of(lo, k);
+  pool_->run_idx(k, [&](std::size_t c, std::size_t lo, std::size_t hi) {
     std::uint64_t *nx = first.data() + c * S;
     std::size_t io = in_b[c], oo = out_b[c];
     noise_gpu_record *recs = sl.recs();

@@ -10,6 +10,9 @@
 //       uploads a large table of new sessions' keys, slot B (another stream,
 //       no upload of its own) is flushed right after with messages of the
 //       last sessions; B's ciphertexts must match the oracle
+//   transport_test resident_race <sessions> [seconds]   Pipeline work on one
+//       thread while another sends resident single-record traffic: the
+//       Pipeline must not wait for the resident instance
 //   transport_test bench <batcher|pipeline> <sessions> <messages> <len> [threads]
 //       host-resident throughput, encrypt then decrypt, GiB/s of plaintext;
 //       threads > 1: Pipeline::submit_batch / copy_out over that many copy threads
@@ -20,9 +23,12 @@
 // chunks, decrypted in ONE batch (one record tampered per 97) and compared.
 #include <hip/hip_runtime_api.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <thread>
 #include <deque>
+#include <functional>
 #include <cstdlib>
 #include <cstring>
 #include <random>
@@ -30,6 +36,7 @@
 #include <vector>
 
 #include "noise_amd/transport.hpp"
+#include "noise_gpu.h"
 
 extern "C" {
 void oracle_noise_encrypt(const uint8_t key[32], uint64_t n, const uint8_t *ad, size_t ad_len,
@@ -166,7 +173,7 @@ static int run_pipeline(int S, int M, std::uint64_t seed) {
 // tiny slots its serial walk
 static int run_pipeline_batch(int S, int M, std::uint64_t seed, std::size_t slot_records = 97,
                               std::size_t slot_bytes = 256 << 10, std::size_t maxlen = 3000,
-                              int maxbatch = 300) {
+                              int maxbatch = 300, int threads = 4) {
   std::mt19937_64 rng(seed);
   int fails = 0;
   auto check = [&](bool c, const char *what, long i) {
@@ -177,7 +184,7 @@ static int run_pipeline_batch(int S, int M, std::uint64_t seed, std::size_t slot
   o.slot_bytes = slot_bytes;
   o.slot_records = slot_records;
   o.depth = 3;
-  o.copy_threads = 4;
+  o.copy_threads = threads;  // > 64 with a byte cut below it: chunks that share a first index
   nt::Pipeline enc(nt::Pipeline::Direction::Encrypt, o), dec(nt::Pipeline::Direction::Decrypt, o);
   std::vector<std::array<std::uint8_t, 32>> keys(S);
   std::vector<std::uint64_t> n0(S);
@@ -291,6 +298,237 @@ static int run_keyrace(int S) {
   (void)ta;
   std::printf("keyrace sessions %d messages %d: %s (%d failures)\n", S, M, fails ? "FAIL" : "ok", fails);
   return fails ? 1 : 0;
+}
+
+// Resident traffic beside batch work: thread A turns on the
+// resident latency mode and sends 1 KiB records back to back (gaps of a few
+// microseconds, far below the instance's idle exit), thread B meanwhile builds
+// a Pipeline, adds S sessions (the key table doubles from 1024 rows up) and
+// encrypts growing batches through it (the records scratch of a slot stream
+// grows), checked against the oracle.  Nothing B does may wait for every
+// stream of the device (hipDeviceSynchronize / hipFree would wait for A's
+// instance, i.e. until A stops): B must finish while A is still sending.
+// Prints B's time and A's record count; fails if B outlived A's traffic.
+static int run_resident_race(int S, double a_max_s) {
+  using clk = std::chrono::steady_clock;
+  int fails = 0;
+  std::atomic<bool> b_done{false};
+  std::atomic<long> a_records{0};
+  std::atomic<int> a_err{0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::thread ta([&] {
+    (void)hipSetDevice(dev);
+    if (noise_gpu_set_resident(1, 0) != NOISE_GPU_OK) {
+      a_err = 1;
+      return;
+    }
+    std::array<std::uint8_t, 32> key{};
+    for (int i = 0; i < 32; ++i) key[i] = (std::uint8_t)(i + 1);
+    bytes buf(1024 + 16), pt(1024), want(1024 + 16);
+    for (std::size_t i = 0; i < pt.size(); ++i) pt[i] = (std::uint8_t)(i * 7);
+    const auto t0 = clk::now();
+    std::uint64_t n = 0;
+    while (!b_done.load() && std::chrono::duration<double>(clk::now() - t0).count() < a_max_s) {
+      std::memcpy(buf.data(), pt.data(), pt.size());
+      if (noise_gpu_encrypt_host(key.data(), n, nullptr, 0, buf.data(), pt.size()) != NOISE_GPU_OK) {
+        a_err = 2;
+        break;
+      }
+      if ((n & 1023u) == 0) {  // now and then against the oracle
+        oracle_noise_encrypt(key.data(), n, nullptr, 0, pt.data(), pt.size(), want.data());
+        if (buf != want) a_err = 3;
+      }
+      ++n;
+      ++a_records;
+    }
+    (void)noise_gpu_set_resident(0, 0);
+  });
+  while (a_records.load() < 200 && !a_err.load()) std::this_thread::yield();
+  const auto t0 = clk::now();
+  double tb = 0;
+  std::vector<double> phase;  // seconds since t0: Pipeline built, sessions added, each flush done
+  {
+    std::mt19937_64 rng(7);
+    nt::Pipeline::Options o;
+    o.slot_bytes = 64 << 20;
+    o.slot_records = 65536;
+    nt::Pipeline enc(nt::Pipeline::Direction::Encrypt, o);
+    phase.push_back(std::chrono::duration<double>(clk::now() - t0).count());
+    std::vector<std::array<std::uint8_t, 32>> keys(S);
+    for (int s = 0; s < S; ++s) {
+      for (auto &b : keys[s]) b = (std::uint8_t)rng();
+      noise::CipherState cs;
+      cs.initialize_key(keys[s]);
+      enc.add_session(cs);
+    }
+    phase.push_back(std::chrono::duration<double>(clk::now() - t0).count());
+    std::vector<std::uint64_t> next(S, 0);
+    bytes pt(4096), want(4096 + 16);
+    for (auto &b : pt) b = (std::uint8_t)rng();
+    // five flushes; the fifth, the largest, lands on the first slot's stream
+    // again and grows its records scratch
+    for (int f = 0; f < 5; ++f) {
+      const int M = f < 4 ? 2500 : 30000;
+      std::vector<int> sess(M);
+      std::vector<std::size_t> len(M);
+      std::vector<std::uint64_t> nonce(M);
+      for (int i = 0; i < M; ++i) {
+        sess[i] = (int)(rng() % S);
+        len[i] = i % 7 == 0 ? 4096 : 1024;
+        nonce[i] = next[sess[i]]++;
+        if (!enc.submit(sess[i], pt.data(), len[i]) && fails++ < 10) std::printf("FAIL submit %d\n", i);
+      }
+      const nt::Pipeline::Batch b = enc.wait(enc.flush());
+      for (int i = 0; i < M; i += 13) {
+        oracle_noise_encrypt(keys[sess[i]].data(), nonce[i], nullptr, 0, pt.data(), len[i], want.data());
+        if (b.length(i) != len[i] + 16 || std::memcmp(b.data(i), want.data(), len[i] + 16) != 0)
+          if (fails++ < 10) std::printf("FAIL record %d of flush %d\n", i, f);
+      }
+      phase.push_back(std::chrono::duration<double>(clk::now() - t0).count());
+    }
+    tb = std::chrono::duration<double>(clk::now() - t0).count();
+    b_done = true;  // A stops; the Pipeline's destructor (hipHostFree) may wait for that
+  }
+  ta.join();
+  if (a_err.load() && fails++ < 10) std::printf("FAIL resident thread error %d\n", a_err.load());
+  if (tb >= a_max_s * 0.9 && fails++ < 10)
+    std::printf("FAIL the Pipeline work took %.2f s: it waited for the resident traffic\n", tb);
+  std::printf("{\"resident_race\": \"%s\", \"sessions\": %d, \"pipeline_s\": %.3f, "
+              "\"resident_records_meanwhile\": %ld, \"failures\": %d, \"phases_s\": [",
+              fails ? "FAIL" : "ok", S, tb, a_records.load(), fails);
+  for (std::size_t i = 0; i < phase.size(); ++i) std::printf("%s%.3f", i ? ", " : "", phase[i]);
+  std::printf("]}\n");
+  return fails ? 1 : 0;
+}
+
+// Which HIP runtime calls wait for a resident instance on another thread's
+// stream?  For each call: start steady resident traffic on a second thread,
+// time the call, stop the traffic (after at most `cap_s`).  A call that
+// waits for every stream of the device takes ~cap_s.
+static int run_resident_probe(double cap_s) {
+  using clk = std::chrono::steady_clock;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  hipStream_t st = nullptr;
+  (void)hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+  struct Op {
+    const char *name;
+    std::function<void()> fn;
+  };
+  void *hp = nullptr, *dp = nullptr, *ap = nullptr;
+  std::vector<Op> ops = {
+      {"hipHostMalloc", [&] { (void)hipHostMalloc(&hp, 64 << 20, hipHostMallocDefault); }},
+      {"hipMalloc", [&] { (void)hipMalloc(&dp, 64 << 20); }},
+      {"hipMallocAsync", [&] { (void)hipMallocAsync(&ap, 64 << 20, st); (void)hipStreamSynchronize(st); }},
+      {"hipMemcpyAsync+streamsync", [&] {
+         (void)hipMemcpyAsync(dp, hp, 1 << 20, hipMemcpyHostToDevice, st);
+         (void)hipStreamSynchronize(st);
+       }},
+      {"hipMemcpy", [&] { (void)hipMemcpy(dp, hp, 1 << 20, hipMemcpyHostToDevice); }},
+      {"hipMemset", [&] { (void)hipMemset(dp, 0, 1 << 20); }},
+      {"hipFreeAsync", [&] { (void)hipFreeAsync(ap, st); (void)hipStreamSynchronize(st); }},
+      {"hipFree", [&] { (void)hipFree(dp); }},
+      {"hipHostFree", [&] { (void)hipHostFree(hp); }},
+      {"hipStreamCreate+Destroy", [&] {
+         hipStream_t s2;
+         (void)hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
+         (void)hipStreamDestroy(s2);
+       }},
+      {"hipStreamCreate+hipMallocAsync+sync", [&] {
+         hipStream_t s2;
+         void *q = nullptr;
+         (void)hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
+         (void)hipMallocAsync(&q, 64 << 20, s2);
+         (void)hipStreamSynchronize(s2);
+         (void)hipFreeAsync(q, s2);
+         (void)hipStreamSynchronize(s2);
+         (void)hipStreamDestroy(s2);
+       }},
+      {"hipStreamCreate x6 + kernel-free sync", [&] {
+         hipStream_t s2[6];
+         for (auto &x : s2) (void)hipStreamCreateWithFlags(&x, hipStreamNonBlocking);
+         for (auto &x : s2) (void)hipStreamSynchronize(x);
+         for (auto &x : s2) (void)hipStreamDestroy(x);
+       }},
+      {"hipEventCreate+Destroy", [&] {
+         hipEvent_t e;
+         (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+         (void)hipEventDestroy(e);
+       }},
+  };
+  int pools = -1;
+  const hipError_t pe = hipDeviceGetAttribute(&pools, hipDeviceAttributeMemoryPoolsSupported, dev);
+  std::printf("{\"resident_probe_cap_s\": %.1f, \"memory_pools_attr\": %d, \"attr_rc\": %d", cap_s, pools,
+              (int)pe);
+  for (const Op &op : ops) {
+    std::atomic<bool> stop{false};
+    std::atomic<long> recs{0};
+    std::thread ta([&] {
+      (void)hipSetDevice(dev);
+      (void)noise_gpu_set_resident(1, 0);
+      std::array<std::uint8_t, 32> key{};
+      key[0] = 1;
+      bytes buf(64 + 16);
+      const auto t0 = clk::now();
+      for (std::uint64_t n = 0; !stop.load() && std::chrono::duration<double>(clk::now() - t0).count() < cap_s; ++n) {
+        (void)noise_gpu_encrypt_host(key.data(), n, nullptr, 0, buf.data(), 64);
+        ++recs;
+      }
+      std::fprintf(stderr, "probe: traffic stops\n");
+      const int rc = noise_gpu_set_resident(0, 0);
+      std::fprintf(stderr, "probe: resident off rc %d (%s)\n", rc, noise_gpu_last_error());
+      if (std::getenv("PROBE_THREAD_RELEASE")) {
+        const int rc2 = noise_gpu_thread_release();
+        std::fprintf(stderr, "probe: thread release rc %d\n", rc2);
+      }
+    });
+    while (recs.load() < 200) std::this_thread::yield();
+    std::fprintf(stderr, "probe: %s ...\n", op.name);
+    const auto t0 = clk::now();
+    op.fn();
+    const double t = std::chrono::duration<double>(clk::now() - t0).count();
+    std::fprintf(stderr, "probe: %s %.4f s (%ld resident records so far)\n", op.name, t, recs.load());
+    stop = true;
+    ta.join();
+    std::fprintf(stderr, "probe: traffic thread joined\n");
+    std::printf(", \"%s\": %.4f", op.name, t);
+    std::fflush(stdout);
+  }
+  std::printf("}\n");
+  (void)hipStreamDestroy(st);
+  return 0;
+}
+
+// A live resident instance for `secs` seconds (tools/gpu/r4_resident_cost.sh
+// runs the batch benches beside it): busy = 1 sends 1 KiB records back to
+// back, busy = 0 one record every 5 ms (the instance stays up, polling).
+static int run_resident_hold(double secs, int busy) {
+  using clk = std::chrono::steady_clock;
+  if (noise_gpu_set_resident(1, 10000000) != NOISE_GPU_OK) return 1;
+  std::array<std::uint8_t, 32> key{};
+  key[0] = 9;
+  bytes buf(1024 + 16);
+  long n = 0;
+  const auto t0 = clk::now();
+  const char *stop_file = std::getenv("RESIDENT_HOLD_STOP");  // leave early once it exists
+  while (std::chrono::duration<double>(clk::now() - t0).count() < secs) {
+    if (noise_gpu_encrypt_host(key.data(), (std::uint64_t)n, nullptr, 0, buf.data(), 1024) != NOISE_GPU_OK)
+      return 2;
+    ++n;
+    if (!busy) std::this_thread::sleep_for(std::chrono::milliseconds(5));
+    if (stop_file && (n & 255) == 0) {
+      if (FILE *f = std::fopen(stop_file, "r")) {
+        std::fclose(f);
+        break;
+      }
+    }
+  }
+  const double t = std::chrono::duration<double>(clk::now() - t0).count();
+  (void)noise_gpu_set_resident(0, 0);
+  std::printf("{\"resident_hold\": %d, \"records\": %ld, \"seconds\": %.2f, \"us_per_record\": %.3f}\n",
+              busy, n, t, t / (double)n * 1e6);
+  return 0;
 }
 
 // Host-resident throughput: M messages of len bytes from one source buffer
@@ -440,11 +678,18 @@ int main(int argc, char **argv) {
   if (argc > 1 && std::string(argv[1]) == "pipeline")
     return run_pipeline(std::atoi(argv[2]), std::atoi(argv[3]), std::strtoull(argv[4], nullptr, 0));
   if (argc > 1 && std::string(argv[1]) == "keyrace") return run_keyrace(std::atoi(argv[2]));
+  if (argc > 1 && std::string(argv[1]) == "resident_hold")
+    return run_resident_hold(std::atof(argv[2]), std::atoi(argv[3]));
+  if (argc > 1 && std::string(argv[1]) == "resident_probe")
+    return run_resident_probe(argc > 2 ? std::atof(argv[2]) : 3.0);
+  if (argc > 1 && std::string(argv[1]) == "resident_race")
+    return run_resident_race(std::atoi(argv[2]), argc > 3 ? std::atof(argv[3]) : 60.0);
   if (argc > 1 && std::string(argv[1]) == "pipeline_batch") {
-    if (argc > 8)  // slot_records slot_bytes maxlen maxbatch
+    if (argc > 8)  // slot_records slot_bytes maxlen maxbatch [copy threads]
       return run_pipeline_batch(std::atoi(argv[2]), std::atoi(argv[3]), std::strtoull(argv[4], nullptr, 0),
                                 std::strtoull(argv[5], nullptr, 0), std::strtoull(argv[6], nullptr, 0),
-                                std::strtoull(argv[7], nullptr, 0), std::atoi(argv[8]));
+                                std::strtoull(argv[7], nullptr, 0), std::atoi(argv[8]),
+                                argc > 9 ? std::atoi(argv[9]) : 4);
     return run_pipeline_batch(std::atoi(argv[2]), std::atoi(argv[3]), std::strtoull(argv[4], nullptr, 0));
   }
   if (argc > 1 && std::string(argv[1]) == "bench")

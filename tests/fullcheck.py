@@ -59,6 +59,56 @@ def check_uniform(oracle, torch, key, n0, d_in, in_stride, d_out, out_stride, le
     return {"records": nrec, "mismatches": 0, "seconds": round(time.time() - t0, 2)}
 
 
+def check_synthetic(oracle, torch, d_buf, nbytes, seed, offset, chunk=CHUNK // 4):
+    """The device buffer holds bytes [offset, offset + nbytes) of the
+    splitmix64 stream `seed` (bench.py's per-rank data offset)."""
+    _sync(torch)
+    h = _Pinned(torch, min(nbytes, chunk))
+    for lo in range(0, nbytes, chunk):
+        hi = min(nbytes, lo + chunk)
+        a = h.fill(d_buf, lo, hi)
+        _sync(torch)
+        want = np.frombuffer(oracle.synthetic(hi - lo, seed, offset=offset + lo), dtype=np.uint8)
+        if not np.array_equal(a, want):
+            bad = int(np.flatnonzero(a != want)[0])
+            raise AssertionError("synthetic data differs at byte %d (stream offset %d)"
+                                 % (lo + bad, offset + lo + bad))
+    return {"bytes": nbytes}
+
+
+def check_bench_shard(oracle, torch, shard):
+    """bench.py --check-oracle: one rank's whole shard after the timed run.
+    `shard` (bench.make_workload's "oracle" entry) names the rank's buffers,
+    its global nonce base and data offset.  Every record is recomputed by the
+    oracle in both directions at the rank's GLOBAL nonces (noise.cpp:207-215,
+    monocypher.c:2891-2929), and the plaintext is checked against the
+    synthetic stream at the rank's global data offset -- an error in either
+    that is the same in both directions round-trips and self-authenticates,
+    so only this check sees it."""
+    kind = shard["kind"]
+    out = {"kind": kind, "nonce_base": int(shard["n_base"])}
+    if kind == "uniform":
+        R, L, n0 = shard["R"], shard["L"], shard["n_base"]
+        out["synthetic"] = check_synthetic(oracle, torch, shard["pt"], R * L, shard["seed"],
+                                           shard["data_offset"])
+        out["encrypt"] = check_uniform(oracle, torch, shard["key"], n0, shard["pt"], L, shard["ct"],
+                                       L + 16, L, R)
+        out["decrypt"] = check_uniform(oracle, torch, shard["key"], n0, shard["ct"], L + 16,
+                                       shard["back"], L, L, R, decrypt=True,
+                                       d_status=shard["status"])
+    else:  # descriptor batches (sessions, records)
+        keys = shard["keys"].cpu().numpy() if hasattr(shard["keys"], "cpu") else shard["keys"]
+        keys = np.ascontiguousarray(keys)
+        if shard.get("seed") is not None:
+            out["synthetic"] = check_synthetic(oracle, torch, shard["pt"], shard["pt_bytes"],
+                                               shard["seed"], shard["data_offset"])
+        enc, dec = shard["descs"]()
+        out["encrypt"] = check_records(oracle, torch, keys, enc, shard["pt"], shard["ct"])
+        out["decrypt"] = check_records(oracle, torch, keys, dec, shard["ct"], shard["back"],
+                                       decrypt=True, d_status=shard["status"])
+    return out
+
+
 def check_records(oracle, torch, keys, desc, d_in, d_out, decrypt=False, d_status=None,
                   chunk=CHUNK):
     """Every descriptor of a batch whose in_off / out_off both increase with

@@ -83,6 +83,9 @@ def test_host_entry_points_emulated_and_wiped():
     ["pipeline_batch", "20", "600", "4"],                 # copy pool, ragged batches
     ["pipeline_batch", "30", "5000", "6", "8192", str(1 << 20), "600", "20000"],  # parallel bookkeeping, byte cut
     ["keyrace", "4096"],                                  # key rows uploaded on another slot's stream
+    # 96 copy threads, 256 KiB slots of ~85 messages: the byte cut leaves fewer
+    # messages than threads (empty chunks must keep their own index)
+    ["pipeline_batch", "40", "6000", "8", "8192", str(256 << 10), "6000", "20000", "96"],
 ])
 def test_transport_pipeline_emulated(args):
     """noise::transport::Pipeline (host/transport.cpp: copy pool, launcher

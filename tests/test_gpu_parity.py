@@ -600,7 +600,7 @@ def test_transport_pipeline(sessions, messages, seed):
 
 
 @pytest.mark.parametrize("sessions,messages,seed,big", [(60, 2500, 5, False), (700, 40000, 6, True),
-                                                       (3, 30000, 7, True)])
+                                                       (3, 30000, 7, True), (40, 30000, 8, "T96")])
 def test_transport_pipeline_batched_copies(sessions, messages, seed, big):
     """Pipeline::submit_batch / copy_out with 4 copy threads: ragged batches
     crossing slot boundaries, ciphertexts vs the oracle, nonce accounting,
@@ -610,6 +610,8 @@ def test_transport_pipeline_batched_copies(sessions, messages, seed, big):
     record and the byte capacity; 3 sessions: long runs per session)."""
     exe = os.path.join(noise_amd.ROOT, "noise-cpp_amd", "bin", "transport_test")
     extra = ["8192", str(2 << 20), "600", "20000"] if big else []
+    if big == "T96":  # 96 copy threads, byte cut below the thread count (ADVICE r3)
+        extra = ["8192", str(256 << 10), "6000", "20000", "96"]
     r = subprocess.run([exe, "pipeline_batch", str(sessions), str(messages), str(seed)] + extra,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
@@ -625,6 +627,26 @@ def test_transport_pipeline_key_upload_order():
     r = subprocess.run([exe, "keyrace", str(1 << 18)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "ok (0 failures)" in r.stdout
+
+
+def test_transport_pipeline_beside_resident_traffic():
+    """one thread sends resident single-record traffic
+    back to back (noise_gpu_set_resident) while another builds a Pipeline,
+    grows its key table three times (1024 -> 8192 rows) and pushes growing
+    batches (a slot stream's records scratch grows).  Key tables, scratch and
+    staging are freed stream-ordered (noise_amd/dev_mem.hpp), so the Pipeline
+    work never waits for the resident instance: it must finish while the
+    resident thread is still sending (which it does for up to 60 s).  Both
+    threads' records are checked against the oracle."""
+    import json
+    exe = os.path.join(noise_amd.ROOT, "noise-cpp_amd", "bin", "transport_test")
+    r = subprocess.run([exe, "resident_race", "5000", "60"], capture_output=True, text=True,
+                       timeout=150)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["resident_race"] == "ok" and line["pipeline_s"] < 30, line
+    assert line["resident_records_meanwhile"] > 1000, line
+    print("resident race:", json.dumps(line))
 
 
 def _sessions_case(rng, nkeys, per, length):

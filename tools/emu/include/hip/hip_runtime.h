@@ -299,6 +299,14 @@ inline hipError_t hipStreamCreateWithFlags(hipStream_t *s, unsigned) {
   *s = reinterpret_cast<hipStream_t>(next.fetch_add(16));
   return hipSuccess;
 }
+inline hipError_t hipDeviceGetStreamPriorityRange(int *least, int *greatest) {
+  *least = 0;
+  *greatest = -1;
+  return hipSuccess;
+}
+inline hipError_t hipStreamCreateWithPriority(hipStream_t *s, unsigned f, int) {
+  return hipStreamCreateWithFlags(s, f);
+}
 inline hipError_t hipEventCreateWithFlags(hipEvent_t *e, unsigned) {
   static int tag;
   *e = &tag;
@@ -345,6 +353,15 @@ inline hipError_t hipFree(void *p) {
   std::free(p);
   return hipSuccess;
 }
+// stream-ordered allocations (noise_amd/dev_mem.hpp): the emulated device has
+// memory pools; launches are synchronous, so the free is immediate
+enum hipDeviceAttribute_t { hipDeviceAttributeMemoryPoolsSupported = 0x2001 };
+inline hipError_t hipDeviceGetAttribute(int *v, hipDeviceAttribute_t, int) {
+  *v = 1;
+  return hipSuccess;
+}
+inline hipError_t hipMallocAsync(void **p, size_t n, hipStream_t) { return hipMalloc(p, n); }
+inline hipError_t hipFreeAsync(void *p, hipStream_t) { return hipFree(p); }
 enum hipMemcpyKind { hipMemcpyHostToDevice, hipMemcpyDeviceToHost, hipMemcpyDeviceToDevice };
 inline hipError_t hipMemset(void *p, int v, size_t n) {
   std::memset(p, v, n);

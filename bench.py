@@ -548,11 +548,11 @@ def make_workload(cfg, args, rank, world, stream):
                 "enc_bytes": pt_bytes + ct_bytes + 48 * R, "dec_bytes": pt_bytes + ct_bytes + 49 * R,
                 "read_bytes": (pt_bytes + 48 * R, ct_bytes + 48 * R),
                 "knames": (("noise_amd::k_cls_", "noise_amd::k_seg_prep", "noise_amd::k_seg_tail<false",
-                            "noise_amd::k_seg_finalize<false", "noise_amd::k_seg_finalize_w<false", "noise_amd::k_aead_tile<false",
+                            "noise_amd::k_seg_finalize_w<false", "noise_amd::k_aead_tile<false",
                             "noise_amd::k_aead_records<false"),
                            ("noise_amd::k_cls_", "noise_amd::k_seg_prep", "noise_amd::k_seg_tail<true",
-                            "noise_amd::k_seg_finalize<true", "noise_amd::k_seg_finalize_w<true", "noise_amd::k_seg_fixup",
-                            "noise_amd::k_aead_tile<true", "noise_amd::k_aead_records<true")),
+                            "noise_amd::k_seg_finalize_w<true", "noise_amd::k_aead_tile<true",
+                            "noise_amd::k_aead_records<true")),
                 "call_level": True, "oracle": oracle}
     else:
         raise SystemExit("unknown config %d" % cfg)

@@ -123,18 +123,17 @@ int noise_gpu_decrypt_uniform(const uint8_t h_key[32], uint64_t nonce0,
  * Batches of >= 2048 records are load-balanced on the device, stream-ordered
  * (no host synchronisation): records are sorted by class and each class
  * runs its own kernel -- 16-byte aligned AD-free records of 64, 128, 192,
- * 256 and 512 bytes on the LDS-staged tile kernel; aligned AD-free records of
- * 1024..65535 bytes (any length) cut into 1 KiB segments that ONE tile-kernel
- * launch processes, plus a tail kernel and a per-record finalize (tag);
- * everything else one lane per record.  The tile classes and the
- * one-lane-per-record path check each tag before they store plaintext.  A
- * segmented (>= 1 KiB) record is the exception: its segments are decrypted
- * in parallel before the record's tag is known, so the plaintext is written
- * first and, when the tag fails, XORed back to the ciphertext (in place) or
- * zeroed (copy) by a fix-up kernel later in the same call.  The final buffer
- * contents follow the rules above; between those kernels the output buffer
- * transiently holds unauthenticated plaintext of a failed record.  Scratch
- * is a grow-only device buffer per (device, stream). */
+ * 256, 512 and 1024 bytes on the LDS-staged tile kernel; aligned AD-free
+ * records of 1024..65535 bytes (any length) cut into 1 KiB segments that ONE
+ * tile-kernel launch processes, plus a tail kernel and a per-record finalize
+ * (tag); everything else one lane per record.  Every path checks a record's
+ * tag before any of its plaintext is stored (crypto_aead_read,
+ * monocypher.c:2912-2929): the tile classes and the one-lane-per-record path
+ * per record; a segmented (>= 1 KiB) record by a Poly1305 pass over its
+ * ciphertext and the finalize's tag check, after which a keystream pass
+ * writes the plaintext of the records that verified -- the output range of a
+ * failed record never holds a byte of its plaintext, not even transiently.
+ * Scratch is a grow-only device buffer per (device, stream). */
 int noise_gpu_encrypt_records(const uint8_t *d_keys, uint32_t nkeys,
                               const noise_gpu_record *d_recs, uint64_t nrec,
                               const uint8_t *d_in, uint8_t *d_out,

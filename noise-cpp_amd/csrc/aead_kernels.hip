@@ -110,8 +110,13 @@ hipError_t launch_aead_uniform(bool decrypt, const uint32_t key[8],
     // packed records (stride == record size on both sides): cheap addressing
     const bool contig = decrypt ? (in_stride == (uint64_t)len + 16 && out_stride == len)
                                 : (in_stride == len && out_stride == (uint64_t)len + 16);
+#ifndef NOISE_UNIFORM_SPAN  // bytes per lane of the uniform tile kernels (A/B: 128)
+#define NOISE_UNIFORM_SPAN 256
+#endif
 #define NOISE_TILE_LAUNCH(DEC, LEN, CONTIG)                                    \
-    hipLaunchKernelGGL((k_aead_tile<DEC, LEN, CONTIG>), gt, bt, 0, stream, ta)
+    hipLaunchKernelGGL((k_aead_tile<DEC, LEN, CONTIG, kTileUniform, 0, 1,       \
+                                    (LEN >= 256 && LEN <= 8192) ? NOISE_UNIFORM_SPAN : 256>), \
+                       gt, bt, 0, stream, ta)
 #define NOISE_TILE_CASE(LEN)                                                   \
     case LEN:                                                                  \
       if (decrypt) {                                                           \

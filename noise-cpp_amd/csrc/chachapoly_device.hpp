@@ -432,6 +432,9 @@ __device__ __forceinline__ uint4 load16(const uint8_t *p, int n) {
 }
 template <bool VEC>
 __device__ __forceinline__ void store16(uint8_t *p, uint4 v, int n) {
+#if defined(NOISE_HIP_EMU)
+  if (emu::store_hook) emu::store_hook(p, &v, VEC ? 16 : n);  // tools/emu: every record store seen
+#endif
   if (VEC) {
     // one aligned global_store_dwordx4 (a plain uint4 store may be
     // re-split by the store merger into misaligned dwordx3/x4 pieces)

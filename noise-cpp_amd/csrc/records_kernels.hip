@@ -15,12 +15,14 @@
 //        - long records: 16-byte aligned, AD-free, 1024 <= len <= 65535
 //          (any length) -> cut into 1 KiB segments + a tail.  k_seg_prep
 //          derives each record's one-time key and r powers, ONE tile-kernel
-//          launch (kTileSeg) encrypts/decrypts every full segment of every
-//          long record -- uniform 1 KiB work units, whatever the size mix --
-//          and k_seg_finalize combines the segments' Poly1305 partial sums,
-//          runs the tail, the length block and the tag (decrypt: verifies,
-//          and k_seg_fixup restores an in-place record / zeroes a copy whose
-//          tag failed);
+//          launch (kTileSeg) encrypts every full segment of every long
+//          record -- uniform 1 KiB work units, whatever the size mix -- and
+//          k_seg_finalize_w combines the segments' Poly1305 partial sums with
+//          the tail's, the length block and the tag.  Decrypt verifies first:
+//          a Poly1305-only pass over the ciphertext (kTileSegPoly, kTailPoly),
+//          the finalize checks every tag, and only then the keystream pass
+//          (kTileSegXor, kTailXor) writes the plaintext of the records that
+//          verified -- no byte of a failed record's plaintext is ever stored;
 //        - generic: everything else (AD, odd lengths < 1 KiB, unaligned, bad
 //          key index, and long records beyond the segment scratch capacity)
 //          -> one lane per record (chachapoly_device.hpp).
@@ -47,6 +49,25 @@ constexpr int kColTails = kNumCls + 1;    // classifier column: long records wit
 constexpr int kColFin0 = kNumCls + 2;     // classifier columns: long records by
 constexpr int kFinBuckets = 6;            // floor(log2(full segments)), 1..63 -> 0..5
 constexpr int kCols = kNumCls + 2 + kFinBuckets;
+// Decrypt pipelines the long records in kSegChunks chunks (launch_classes):
+// the Poly1305 pass of chunk c + 1 (HBM-bound) runs beside the keystream pass
+// of chunk c (VALU-bound).  Chunk boundaries fall on record starts, near
+// c * nseg / kSegChunks segments.
+#ifndef NOISE_SEG_CHUNKS
+#define NOISE_SEG_CHUNKS 4
+#endif
+constexpr int kSegChunks = NOISE_SEG_CHUNKS;
+// finalize lanes per long record
+#ifndef NOISE_FIN_W
+#define NOISE_FIN_W 4
+#endif
+// The XOR pass's span per lane: 128 B halves its LDS tile (8 segments, 8 KiB)
+// so that, at its ~120 VGPRs, four waves fit per SIMD (256 B: 16.6 KiB per
+// wave, 2.25 waves per SIMD by LDS).  Same box, config 4 (round 4):
+// 3.54-3.61 ms per decrypt against 3.83-3.90 at 256 B.
+#ifndef NOISE_XOR_SPAN
+#define NOISE_XOR_SPAN 128
+#endif
 #ifndef NOISE_CLASSIFY_MIN  // overridable for the CPU emulation build
 #define NOISE_CLASSIFY_MIN 2048
 #endif
@@ -102,8 +123,12 @@ struct RecHdr {
   unsigned long long cls_base[kCols];  // start of each class in idx
   unsigned long long nlong;            // long records handled as segments
   unsigned long long nseg;             // their full segments
-  unsigned long long nfail;            // decrypt: long records whose tag failed
-  unsigned long long pad[61 - 2 * kCols];
+  unsigned long long spare0;
+  // chunk c = long records [qsplit[c], qsplit[c + 1]) = segments [ssplit[c],
+  // ssplit[c + 1]) (k_cls_scatter; clamped to nlong / nseg where used)
+  // and tails [tsplit[c], tsplit[c + 1]) (clamped to the tail count)
+  unsigned long long qsplit[kSegChunks + 1], ssplit[kSegChunks + 1], tsplit[kSegChunks + 1];
+  unsigned long long pad[61 - 2 * kCols - 3 * (kSegChunks + 1)];
 };
 static_assert(sizeof(RecHdr) == 512, "scratch header layout");
 
@@ -213,9 +238,18 @@ __global__ __launch_bounds__(64) void k_cls_scan(const uint32_t *part, uint32_t 
     // lowered by k_cls_scatter if the segment scratch overflows
     if (c == (uint32_t)kClsLong) {
       hdr->nlong = run;
-      hdr->nfail = 0;
+      hdr->spare0 = 0;
     }
-    if (c == (uint32_t)kColSegs) hdr->nseg = run < segcap ? run : segcap;
+    if (c == (uint32_t)kColSegs) {
+      hdr->nseg = run < segcap ? run : segcap;
+      // chunk c >= 1 starts at the record holding segment c * nseg / chunks
+      // (k_cls_scatter writes it; none holds it when there are no segments)
+      for (int k = 0; k <= kSegChunks; ++k) {
+        hdr->qsplit[k] = k == 0 ? 0ull : ~0ull;
+        hdr->ssplit[k] = k == 0 ? 0ull : ~0ull;
+        hdr->tsplit[k] = k == 0 ? 0ull : ~0ull;
+      }
+    }
   }
 }
 
@@ -291,12 +325,12 @@ __global__ __launch_bounds__(64) void k_cls_scatter(
         run[kColFin0 + b] += (unsigned long long)__builtin_popcountll(m);
       }
     }
+    unsigned long long tpos;  // tails of the records before this lane's
     {  // long records with a tail: the tail list (record order)
       const uint64_t m = __ballot(tail);
-      if (tail)
-        tails[run[kColTails] + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
-            (uint32_t)q;
+      tpos = run[kColTails] + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (tail) tails[tpos] = (uint32_t)q;
       run[kColTails] += (unsigned long long)__builtin_popcountll(m);
     }
     // long records: header fields of their SegRec, first segment index
@@ -318,6 +352,16 @@ __global__ __launch_bounds__(64) void k_cls_scatter(
         overflow = true;
         ov_q = q < ov_q ? q : ov_q;
         ov_seg = seg0 < ov_seg ? seg0 : ov_seg;
+      }
+      const unsigned long long total = hdr->counts[kColSegs];
+#pragma unroll
+      for (int k = 1; k < kSegChunks; ++k) {  // the record holding a chunk's first segment
+        const unsigned long long b = total * (unsigned long long)k / kSegChunks;
+        if (seg0 <= b && b < seg0 + nf) {
+          hdr->qsplit[k] = q;
+          hdr->ssplit[k] = seg0;
+          hdr->tsplit[k] = tpos;
+        }
       }
     }
     // segment list entries (q, s), written cooperatively: entry k of this
@@ -393,41 +437,65 @@ __global__ __launch_bounds__(64) void k_seg_prep(const uint8_t *__restrict__ key
 }
 
 // k_seg_tail: lane per tail (a long record's len % 1024 bytes past its last
-// full segment; ChaCha counters from 1 + 16 nfull).  Encrypts / decrypts the
-// tail and leaves its Poly1305 sum P_tail (Horner from 0 over the tail's
-// ciphertext blocks, the last one zero padded) in the SegRec.  Decrypt
-// writes the plaintext unconditionally, like the segment kernel: k_seg_fixup
-// reverts a record whose tag fails.
-template <bool DECRYPT>
+// full segment; ChaCha counters from 1 + 16 nfull), in one of three passes:
+//   kTailFused (encrypt): encrypts the tail and leaves its Poly1305 sum
+//     P_tail (Horner from 0 over the tail's ciphertext blocks, the last one
+//     zero padded) in the SegRec;
+//   kTailPoly (decrypt, before the tag is known): P_tail of the ciphertext
+//     only -- nothing is written to the output;
+//   kTailXor (decrypt, after k_seg_finalize_w): the plaintext of a tail whose
+//     record verified; a failed record's tail is left alone (in place) or
+//     zeroed (copy), as crypto_aead_read leaves a failed record's output.
+enum TailPass : int { kTailFused = 0, kTailPoly = 1, kTailXor = 2 };
+template <bool DECRYPT, int PASS>
 __global__ __launch_bounds__(64) void k_seg_tail(const uint32_t *__restrict__ tails,
                                                  SegRec *rt, const RecHdr *hdr,
-                                                 const uint8_t *in, uint8_t *out) {
-  const uint64_t n = hdr->counts[kColTails], nlong = hdr->nlong;
+                                                 const uint8_t *in, uint8_t *out, int chunk) {
+  static_assert(PASS == kTailFused || DECRYPT, "split tail passes are decrypt's");
+  constexpr bool XOR = PASS != kTailPoly, POLY = PASS != kTailXor;
+  const uint64_t nall = hdr->counts[kColTails], nlong = hdr->nlong;
+  uint64_t t0 = 0, n = nall;  // chunk c: the tails [tsplit[c], tsplit[c + 1])
+  if (chunk >= 0) {
+    const uint64_t lo = hdr->tsplit[chunk], hi = hdr->tsplit[chunk + 1];
+    t0 = lo < nall ? lo : nall;
+    n = hi < nall ? hi : nall;
+  }
 #pragma unroll 1
-  for (uint64_t t = (uint64_t)blockIdx.x * 64 + threadIdx.x; t < n;
+  for (uint64_t t = t0 + (uint64_t)blockIdx.x * 64 + threadIdx.x; t < n;
        t += (uint64_t)gridDim.x * 64) {
     const uint32_t q = tails[t];
     if (q >= nlong) continue;  // beyond the segment scratch: generic kernel
     SegRec &R = rt[q];
-    uint32_t k[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) k[i] = R.k[i];
-    Poly1305 p;
-    p.r0 = R.r[0]; p.r1 = R.r[1]; p.r2 = R.r[2]; p.r3 = R.r[3];
-    p.rr0 = (p.r0 >> 2) * 5u;
-    p.rr1 = p.r1 + (p.r1 >> 2);
-    p.rr2 = p.r2 + (p.r2 >> 2);
-    p.rr3 = p.r3 + (p.r3 >> 2);
-    p.r0lo = p.r0 & 3u;
-    p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0u;
     const uint32_t nf = R.nfull, tb = R.len - 1024u * nf;
     const uint8_t *src = in + R.in_off + 1024ull * nf;
     uint8_t *dst = out + R.out_off + 1024ull * nf;
+    if (PASS == kTailXor && !R.ok) {  // the tag failed: no plaintext leaves
+      if (in + R.in_off != out + R.out_off)
+        for (uint32_t off = 0; off < tb; off += 16) {
+          const int nb = tb - off >= 16u ? 16 : (int)(tb - off);
+          if (nb == 16) store16<true>(dst + off, make_uint4(0u, 0u, 0u, 0u), 16);
+          else store16<false>(dst + off, make_uint4(0u, 0u, 0u, 0u), nb);
+        }
+      continue;
+    }
+    uint32_t k[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) k[i] = XOR ? R.k[i] : 0u;
+    Poly1305 p;
+    p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0u;
+    if (POLY) {
+      p.r0 = R.r[0]; p.r1 = R.r[1]; p.r2 = R.r[2]; p.r3 = R.r[3];
+      p.rr0 = (p.r0 >> 2) * 5u;
+      p.rr1 = p.r1 + (p.r1 >> 2);
+      p.rr2 = p.r2 + (p.r2 >> 2);
+      p.rr3 = p.r3 + (p.r3 >> 2);
+      p.r0lo = p.r0 & 3u;
+    }
     const uint32_t n_lo = (uint32_t)R.nonce, n_hi = (uint32_t)(R.nonce >> 32);
 #pragma unroll 1
     for (uint32_t off = 0; off < tb; off += 64) {
       uint32_t ks[16];
-      chacha20_block(k, 1u + 16u * nf + (off >> 6), n_lo, n_hi, ks);
+      if (XOR) chacha20_block(k, 1u + 16u * nf + (off >> 6), n_lo, n_hi, ks);
       uint4 v[4];
 #pragma unroll
       for (int w = 0; w < 4; ++w) {  // the chunk's loads first (independent)
@@ -441,119 +509,30 @@ __global__ __launch_bounds__(64) void k_seg_tail(const uint32_t *__restrict__ ta
         const int m = (int)(tb - off) - 16 * w;
         if (m <= 0) break;
         const int nb = m >= 16 ? 16 : m;
+        if (POLY && DECRYPT) poly_block(p, v[w].x, v[w].y, v[w].z, v[w].w);
+        if (!XOR) continue;
         const uint4 o = mask_bytes(make_uint4(v[w].x ^ ks[4 * w], v[w].y ^ ks[4 * w + 1],
                                               v[w].z ^ ks[4 * w + 2], v[w].w ^ ks[4 * w + 3]), nb);
-        if (DECRYPT) poly_block(p, v[w].x, v[w].y, v[w].z, v[w].w);
-        else poly_block(p, o.x, o.y, o.z, o.w);
+        if (POLY && !DECRYPT) poly_block(p, o.x, o.y, o.z, o.w);
         if (nb == 16) store16<true>(dst + off + 16 * w, o, 16);
         else store16<false>(dst + off + 16 * w, o, nb);
       }
     }
-    R.ptail[0] = p.h0; R.ptail[1] = p.h1; R.ptail[2] = p.h2; R.ptail[3] = p.h3;
-    R.ptail[4] = p.h4;
-  }
-}
-
-// k_seg_finalize: lane per long record, in finalize order (the classifier's
-// segment-count buckets: a wave's records loop over similar segment counts,
-// not up to the longest record of a random mix).  h = Horner over the
-// segments' partial sums in R = r^64, then h r^(tail blocks) + P_tail, the
-// length block and the tag.  Encrypt stores the tag; decrypt compares it and
-// writes the record's status.
-template <bool DECRYPT>
-__global__ __launch_bounds__(64) void k_seg_finalize(
-    const uint32_t *__restrict__ fin, const SegRec *__restrict__ rt,
-    const SegPartial *__restrict__ partial, const uint32_t *__restrict__ partial_hi,
-    const RecHdr *hdr, const uint8_t *in, uint8_t *out, uint8_t *status) {
-  const uint64_t n = hdr->counts[kClsLong], nlong = hdr->nlong;
-#pragma unroll 1
-  for (uint64_t t = (uint64_t)blockIdx.x * 64 + threadIdx.x; t < n;
-       t += (uint64_t)gridDim.x * 64) {
-    const uint32_t q = fin[t];
-    if (q >= nlong) continue;  // beyond the segment scratch: generic kernel
-    const SegRec &R = rt[q];
-    F26 R64, acc;
-#pragma unroll
-    for (int i = 0; i < 5; ++i) R64.a[i] = R.r64[i];
-    const uint32_t nf = R.nfull;
-    {
-      const SegPartial &P0 = partial[R.seg0];
-      acc = to26(P0.h[0], P0.h[1], P0.h[2], P0.h[3], partial_hi[R.seg0]);
-    }
-    // Horner in R over the partial sums, 8 segments per step: the 8 loads
-    // are issued together (the loop is load-latency bound otherwise: one
-    // dependent round trip per segment, up to 63 per record)
-    uint32_t s = 1;
-#pragma unroll 1
-    for (; s + 8 <= nf; s += 8) {
-      uint4 lo[8];
-      uint32_t hi[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const SegPartial &P = partial[R.seg0 + s + j];
-        lo[j] = make_uint4(P.h[0], P.h[1], P.h[2], P.h[3]);
-        hi[j] = partial_hi[R.seg0 + s + j];
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        acc = mul26(acc, R64);
-        const F26 t = to26(lo[j].x, lo[j].y, lo[j].z, lo[j].w, hi[j]);
-#pragma unroll
-        for (int i = 0; i < 5; ++i) acc.a[i] += t.a[i];
-        carry26(acc);
-      }
-    }
-#pragma unroll 1
-    for (; s < nf; ++s) {
-      const SegPartial &P = partial[R.seg0 + s];
-      acc = mul26(acc, R64);
-      const F26 t = to26(P.h[0], P.h[1], P.h[2], P.h[3], partial_hi[R.seg0 + s]);
-#pragma unroll
-      for (int i = 0; i < 5; ++i) acc.a[i] += t.a[i];
-      carry26(acc);
-    }
-    const uint32_t len = R.len;
-    if (len & 1023u) {
-      F26 rtp;
-#pragma unroll
-      for (int i = 0; i < 5; ++i) rtp.a[i] = R.rtail[i];
-      acc = mul26(acc, rtp);
-      const F26 t = to26(R.ptail[0], R.ptail[1], R.ptail[2], R.ptail[3], R.ptail[4]);
-#pragma unroll
-      for (int i = 0; i < 5; ++i) acc.a[i] += t.a[i];
-    }
-    carry26(acc);
-    carry26(acc);
-    Poly1305 p;
-    from26(acc, p.h0, p.h1, p.h2, p.h3, p.h4);
-    p.r0 = R.r[0]; p.r1 = R.r[1]; p.r2 = R.r[2]; p.r3 = R.r[3];
-    p.rr0 = (p.r0 >> 2) * 5u;
-    p.rr1 = p.r1 + (p.r1 >> 2);
-    p.rr2 = p.r2 + (p.r2 >> 2);
-    p.rr3 = p.r3 + (p.r3 >> 2);
-    p.r0lo = p.r0 & 3u;
-    p.s0 = R.s[0]; p.s1 = R.s[1]; p.s2 = R.s[2]; p.s3 = R.s[3];
-    poly_block(p, 0u, 0u, len, 0u);  // LE64(ad_len = 0) || LE64(len)
-    uint32_t tag[4];
-    poly_final(p, tag);
-    if (!DECRYPT) {
-      uint8_t *tp = out + R.out_off + len;
-      if ((len & 15u) == 0) store16<true>(tp, make_uint4(tag[0], tag[1], tag[2], tag[3]), 16);
-      else store16<false>(tp, make_uint4(tag[0], tag[1], tag[2], tag[3]), 16);
-    } else {
-      const uint8_t *tp = in + R.in_off + len;
-      const uint4 want = (len & 15u) == 0 ? load16<true>(tp, 16) : load16<false>(tp, 16);
-      const uint32_t diff = (want.x ^ tag[0]) | (want.y ^ tag[1]) | (want.z ^ tag[2]) |
-                            (want.w ^ tag[3]);
-      status[R.di] = diff == 0u ? NOISE_GPU_REC_OK : NOISE_GPU_REC_BAD_MAC;
+    if (POLY) {
+      R.ptail[0] = p.h0; R.ptail[1] = p.h1; R.ptail[2] = p.h2; R.ptail[3] = p.h3;
+      R.ptail[4] = p.h4;
     }
   }
 }
 
-// k_seg_finalize_w: the same result with W lanes per long record (a group;
-// a wave finalizes 64 / W records of similar segment count per pass), so a
-// 63-segment record is not one lane's chain of 63 dependent products and
-// load round trips.  Group lane i takes segments i, i + W, ... (loaded
+// k_seg_finalize_w: W lanes per long record (a group; a wave finalizes 64 / W
+// records of similar segment count per pass -- the classifier's segment-count
+// buckets -- so a 63-segment record is not one lane's chain of 63 dependent
+// products and load round trips).  h = the Horner sum of the segments'
+// partial sums in R = r^64, then h r^(tail blocks) + P_tail, the length block
+// and the tag: encrypt stores it; decrypt compares it, writes the record's
+// status and its SegRec.ok, which the plaintext passes (kTileSegXor,
+// kTailXor) read.  Group lane i takes segments i, i + W, ... (loaded
 // together) and runs Horner in R^W:
 //   acc_i = sum_k P_{i+Wk} R^(W(K_i-1-k)),   K_i = ceil((nf - i) / W)
 // then h = sum_i acc_i R^(e_i) with e_i = nf-1 - (i + W(K_i-1)) in [0, W)
@@ -562,17 +541,24 @@ __global__ __launch_bounds__(64) void k_seg_finalize(
 // tag exactly as k_seg_finalize does.  Every lane repeats the log2 W
 // squarings, so W trades chain length for redundant products: W = 4 keeps
 // the whole call cheaper than one lane per record (W = 8 is VALU-bound on
-// the squarings).  Decrypt counts failed tags in hdr->nfail so that
-// k_seg_fixup can return at once when there are none.
+// the squarings).
 template <bool DECRYPT, int W>
 __global__ __launch_bounds__(64) void k_seg_finalize_w(
-    const uint32_t *__restrict__ fin, const SegRec *__restrict__ rt,
+    const uint32_t *__restrict__ fin, SegRec *__restrict__ rt,
     const SegPartial *__restrict__ partial, const uint32_t *__restrict__ partial_hi,
-    RecHdr *hdr, const uint8_t *in, uint8_t *out, uint8_t *status) {
+    RecHdr *hdr, const uint8_t *in, uint8_t *out, uint8_t *status, int chunk) {
   static_assert(W == 2 || W == 4 || W == 8, "lanes per record");
   constexpr int LOGW = W == 2 ? 1 : (W == 4 ? 2 : 3);
   constexpr uint32_t KMAX = (63u + W - 1u) / W;  // segments per lane (nf <= 63)
-  const uint64_t n = hdr->counts[kClsLong], nlong = hdr->nlong;
+  const uint64_t nlong = hdr->nlong;
+  // chunk < 0: every long record, in the classifier's bucket order (fin);
+  // chunk c: the records [qsplit[c], qsplit[c + 1]) in record order
+  uint64_t n = hdr->counts[kClsLong], q0 = 0;
+  if (chunk >= 0) {
+    const uint64_t lo = hdr->qsplit[chunk], hi = hdr->qsplit[chunk + 1];
+    q0 = lo < nlong ? lo : nlong;
+    n = (hi < nlong ? hi : nlong) - q0;
+  }
   const uint32_t i = threadIdx.x & (W - 1u);
 #pragma unroll 1
   for (uint64_t base = (uint64_t)blockIdx.x * (64 / W); base < n;
@@ -580,7 +566,7 @@ __global__ __launch_bounds__(64) void k_seg_finalize_w(
     // every lane stays in the loop body (the butterfly reads all group
     // lanes); a group without a record works on zeros and stores nothing
     const uint64_t t = base + (threadIdx.x / W);
-    uint32_t q = t < n ? fin[t] : 0xffffffffu;
+    uint32_t q = t < n ? (chunk >= 0 ? (uint32_t)(q0 + t) : fin[t]) : 0xffffffffu;
     const bool ok = q < nlong;
     if (!ok) q = 0;
     uint32_t nf = 0;
@@ -639,7 +625,7 @@ __global__ __launch_bounds__(64) void k_seg_finalize_w(
       for (int m = 0; m < 5; ++m) acc.a[m] += (uint32_t)__shfl_xor((int)acc.a[m], b);
     }
     if (i != 0 || !ok) continue;
-    const SegRec &R = rt[q];
+    SegRec &R = rt[q];
     const uint32_t len = R.len;
     if (len & 1023u) {
       carry26(acc);
@@ -675,66 +661,7 @@ __global__ __launch_bounds__(64) void k_seg_finalize_w(
       const uint32_t diff = (want.x ^ tag[0]) | (want.y ^ tag[1]) | (want.z ^ tag[2]) |
                             (want.w ^ tag[3]);
       status[R.di] = diff == 0u ? NOISE_GPU_REC_OK : NOISE_GPU_REC_BAD_MAC;
-      if (diff) atomicAdd(&hdr->nfail, 1ull);
-    }
-  }
-}
-
-// k_seg_fixup (decrypt): lane per full segment, then lane per tail.  The
-// segment and tail kernels wrote plaintext before the tag was known; for a
-// record whose tag failed, put the ciphertext back (in place: XOR the
-// keystream again, leaving the buffer as it was -- crypto_aead_read
-// semantics) or zero the copy.
-__global__ __launch_bounds__(64) void k_seg_fixup(
-    const SegEntry *__restrict__ segs, const uint32_t *__restrict__ tails,
-    const SegRec *__restrict__ rt, const RecHdr *hdr, const uint8_t *in,
-    uint8_t *out, const uint8_t *status) {
-#ifndef NOISE_FIN_LANE
-  if (hdr->nfail == 0) return;  // every long record verified (k_seg_finalize_w)
-#endif
-  const uint64_t nseg = hdr->nseg, ntail = hdr->counts[kColTails], nlong = hdr->nlong;
-#pragma unroll 1
-  for (uint64_t g = (uint64_t)blockIdx.x * 64 + threadIdx.x; g < nseg + ntail;
-       g += (uint64_t)gridDim.x * 64) {
-    uint32_t q, c0, nbytes;
-    if (g < nseg) {
-      const SegEntry e = segs[g];
-      q = e.q;
-      c0 = 16u * e.s;
-      nbytes = 1024u;
-    } else {
-      q = tails[g - nseg];
-      if (q >= nlong) continue;
-      c0 = 16u * rt[q].nfull;
-      nbytes = rt[q].len & 1023u;
-    }
-    const SegRec &R = rt[q];
-    if (status[R.di] == NOISE_GPU_REC_OK) continue;
-    uint8_t *dst = out + R.out_off + 64ull * c0;
-    const bool in_place = in + R.in_off == out + R.out_off;
-    uint32_t k[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) k[i] = R.k[i];
-#pragma unroll 1
-    for (uint32_t off = 0; off < nbytes; off += 64) {
-      uint32_t ks[16];
-      if (in_place)
-        chacha20_block(k, 1u + c0 + (off >> 6), (uint32_t)R.nonce, (uint32_t)(R.nonce >> 32), ks);
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        const int m = (int)(nbytes - off) - 16 * w;
-        if (m <= 0) break;
-        const int nb = m >= 16 ? 16 : m;
-        uint4 o = make_uint4(0u, 0u, 0u, 0u);
-        if (in_place) {
-          const uint4 v = nb == 16 ? load16<true>(dst + off + 16 * w, 16)
-                                   : load16<false>(dst + off + 16 * w, nb);
-          o = make_uint4(v.x ^ ks[4 * w], v.y ^ ks[4 * w + 1], v.z ^ ks[4 * w + 2],
-                         v.w ^ ks[4 * w + 3]);
-        }
-        if (nb == 16) store16<true>(dst + off + 16 * w, o, 16);
-        else store16<false>(dst + off + 16 * w, o, nb);
-      }
+      R.ok = diff == 0u ? 1u : 0u;  // the plaintext passes write only verified records
     }
   }
 }
@@ -890,8 +817,14 @@ static inline unsigned capped(uint64_t want, uint64_t cap) {
 // two independent branches after the classifier (below); the short ones run
 // on the companion stream while the segment kernel fills the GPU.
 struct AuxStream {
-  hipStream_t aux = nullptr;
-  hipEvent_t fork = nullptr, prep = nullptr, join = nullptr;
+  hipStream_t aux = nullptr;   // companion: small classes, generic, tails
+  hipStream_t aux2 = nullptr;  // decrypt: per chunk, tag check + plaintext pass
+  // fork: classifier done; prep: k_seg_prep done; join: encrypt: the
+  // companion branch done, decrypt: the tails' Poly1305 done; join2: the
+  // companion done (decrypt); xdone: the last plaintext pass done; poly[c] /
+  // fin[c]: chunk c's Poly1305 pass / tag check done
+  hipEvent_t fork = nullptr, prep = nullptr, join = nullptr, join2 = nullptr, xdone = nullptr;
+  hipEvent_t poly[kSegChunks] = {}, fin[kSegChunks] = {};
 };
 struct AuxEntry {
   int dev;
@@ -915,9 +848,12 @@ static hipError_t aux_get(AuxStream *out, hipStream_t stream) {
     }
   AuxStream a;
   if ((e = hipStreamCreateWithFlags(&a.aux, hipStreamNonBlocking)) != hipSuccess) return e;
-  if ((e = hipEventCreateWithFlags(&a.fork, hipEventDisableTiming)) != hipSuccess) return e;
-  if ((e = hipEventCreateWithFlags(&a.join, hipEventDisableTiming)) != hipSuccess) return e;
-  if ((e = hipEventCreateWithFlags(&a.prep, hipEventDisableTiming)) != hipSuccess) return e;
+  if ((e = hipStreamCreateWithFlags(&a.aux2, hipStreamNonBlocking)) != hipSuccess) return e;
+  for (hipEvent_t *ev : {&a.fork, &a.join, &a.prep, &a.join2, &a.xdone})
+    if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return e;
+  for (int c = 0; c < kSegChunks; ++c)
+    for (hipEvent_t *ev : {&a.poly[c], &a.fin[c]})
+      if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return e;
   cache.push_back({dev, stream, a});
   *out = a;
   return hipSuccess;
@@ -937,26 +873,48 @@ static hipError_t aux_release(int dev, hipStream_t stream) {
       }
   }
   if (!found) return hipSuccess;
-  hipError_t e = hipStreamSynchronize(a.aux);
-  hipError_t e2 = hipStreamDestroy(a.aux);
-  if (e == hipSuccess) e = e2;
-  for (hipEvent_t ev : {a.fork, a.prep, a.join}) {
+  hipError_t e = hipSuccess, e2;
+  for (hipStream_t st : {a.aux, a.aux2}) {
+    e2 = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = e2;
+    e2 = hipStreamDestroy(st);
+    if (e == hipSuccess) e = e2;
+  }
+  for (hipEvent_t ev : {a.fork, a.prep, a.join, a.join2, a.xdone}) {
     e2 = hipEventDestroy(ev);
     if (e == hipSuccess) e = e2;
   }
+  for (int c = 0; c < kSegChunks; ++c)
+    for (hipEvent_t ev : {a.poly[c], a.fin[c]}) {
+      e2 = hipEventDestroy(ev);
+      if (e == hipSuccess) e = e2;
+    }
   return e;
 }
 
-// After the classifier, two branches:
-//   caller stream : k_seg_prep -+-> segment tile kernel ----- join -> finalize
-//                               |                                   (-> fixup)
+// After the classifier, two branches.  Encrypt:
+//   caller stream : k_seg_prep -+-> segment tile kernel (kTileSeg) --- join -> finalize
 //   companion     : (fork)  the five small tile classes, the generic kernel,
-//                   (wait prep) the tails ------------------------^
+//                   (wait prep) the tails (kTailFused) ------------^
 // The segment kernel is the long pole (~80 % of a config-4 call); the
 // companion branch's launches are short or under-filled (the tails kernel has
 // one lane per tail) and overlap it instead of following it.  The tails go
 // last so their long per-lane chains fill the segment kernel's drain
 // (profiles/round2/ab/ab_experiments.md).
+//
+// Decrypt checks every long record's tag BEFORE any of its plaintext is
+// written (crypto_aead_read, monocypher.c:2912-2929): a Poly1305 pass reads
+// the ciphertext, the finalize checks the tags, then a keystream pass writes
+// the plaintext of the records that verified.  The Poly1305 pass is
+// HBM-bound (it moves the ciphertext once for ~15 % of the arithmetic) and
+// the keystream pass VALU-bound, so the long records go through in
+// kSegChunks chunks and the Poly1305 pass of chunk c + 1 runs beside the
+// tag check and keystream pass of chunk c:
+//   caller     : prep -> Poly(0) -> Poly(1) -> ... -> Poly(K-1)           (wait xdone, join2)
+//   companion  : (fork) small classes, generic, (wait prep) tail Poly1305 -> join
+//                                     ... (wait fin) tail plaintext -> join2
+//   companion 2: (wait join) (wait poly[c]) finalize(c) -> XOR(c), c = 0 .. K-1;
+//                fin after finalize(K-1), xdone after XOR(K-1)
 template <bool DECRYPT>
 static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr *hdr,
                                  const uint8_t *keys, uint32_t nkeys,
@@ -970,6 +928,7 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   if (e != hipSuccess) return e;
 #ifdef NOISE_RECORDS_SERIAL  // diagnostics only: every kernel on the caller's stream
   ax.aux = stream;
+  ax.aux2 = stream;
 #endif
   const dim3 bt(64);
   const dim3 grid(capped((nrec + 63) / 64, NOISE_GRID_CAP));
@@ -980,46 +939,72 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   if ((e = hipStreamWaitEvent(ax.aux, ax.fork, 0)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_seg_prep, grid, bt, 0, stream, keys, rt, hdr);
   if ((e = hipEventRecord(ax.prep, stream)) != hipSuccess) return e;
-  // companion branch: dense tile classes first, the long-latency tails last
-  // (they then overlap the segment kernel's drain; tails first: -3..5 %)
   TileArgs a = ta;
+  const uint64_t gblocks = (nrec + kGenBlock - 1) / kGenBlock;
+  const dim3 gg((unsigned)(gblocks < 2 * NOISE_GRID_CAP ? gblocks : 2 * NOISE_GRID_CAP));
+  const dim3 gseg(capped((segbound + 63) / 64, NOISE_GRID_CAP));
+  const dim3 gfin(capped((nrec + 64 / NOISE_FIN_W - 1) / (64 / NOISE_FIN_W), NOISE_GRID_CAP));
+  RecHdr *hdr_w = const_cast<RecHdr *>(hdr);
+#define NOISE_DESC_TILES()                                                     \
+  NOISE_DESC_TILE(0, 64)                                                       \
+  NOISE_DESC_TILE(1, 128)                                                      \
+  NOISE_DESC_TILE(2, 192)                                                      \
+  NOISE_DESC_TILE(3, 256)                                                      \
+  NOISE_DESC_TILE(4, 512)                                                      \
+  NOISE_DESC_TILE(5, 1024)                                                     \
+  hipLaunchKernelGGL((k_aead_records<DECRYPT>), gg, dim3(kGenBlock), 0, ax.aux, keys, nkeys, recs,  \
+                     nrec, idx, hdr, in, out, ad, status);
 #define NOISE_DESC_TILE(C, LEN)                                                \
   a.cls = C;                                                                   \
   hipLaunchKernelGGL((k_aead_tile<DECRYPT, LEN, false, kTileDesc>), grid, bt, 0, ax.aux, a);
-  NOISE_DESC_TILE(0, 64)
-  NOISE_DESC_TILE(1, 128)
-  NOISE_DESC_TILE(2, 192)
-  NOISE_DESC_TILE(3, 256)
-  NOISE_DESC_TILE(4, 512)
-  NOISE_DESC_TILE(5, 1024)
-#undef NOISE_DESC_TILE
-  const uint64_t gblocks = (nrec + kGenBlock - 1) / kGenBlock;
-  const dim3 gg((unsigned)(gblocks < 2 * NOISE_GRID_CAP ? gblocks : 2 * NOISE_GRID_CAP));
-  hipLaunchKernelGGL((k_aead_records<DECRYPT>), gg, dim3(kGenBlock), 0, ax.aux, keys, nkeys, recs,
-                     nrec, idx, hdr, in, out, ad, status);
-  if ((e = hipStreamWaitEvent(ax.aux, ax.prep, 0)) != hipSuccess) return e;
-  hipLaunchKernelGGL((k_seg_tail<DECRYPT>), grid, bt, 0, ax.aux, tails, rt, hdr, in, out);
-  if ((e = hipEventRecord(ax.join, ax.aux)) != hipSuccess) return e;
-  // caller-stream branch: every full segment of every long record
-  const dim3 gseg(capped((segbound + 63) / 64, NOISE_GRID_CAP));
-  hipLaunchKernelGGL((k_aead_tile<DECRYPT, 1024, false, kTileSeg>), gseg, bt, 0, stream, a);
-  if ((e = hipStreamWaitEvent(stream, ax.join, 0)) != hipSuccess) return e;
-#ifdef NOISE_FIN_LANE  // A/B: one lane per long record
-  hipLaunchKernelGGL((k_seg_finalize<DECRYPT>), grid, bt, 0, stream, fin, ta.rt, ta.partial,
-                     ta.partial_hi, hdr, in, out, status);
-#else
-#ifndef NOISE_FIN_W
-#define NOISE_FIN_W 4
-#endif
-  const dim3 gfin(capped((nrec + 64 / NOISE_FIN_W - 1) / (64 / NOISE_FIN_W), NOISE_GRID_CAP));
-  hipLaunchKernelGGL((k_seg_finalize_w<DECRYPT, NOISE_FIN_W>), gfin, bt, 0, stream, fin, ta.rt,
-                     ta.partial, ta.partial_hi, const_cast<RecHdr *>(hdr), in, out, status);
-#endif
-  if (DECRYPT) {
-    const dim3 gfix(capped((segbound + nrec + 63) / 64, NOISE_GRID_CAP));
-    hipLaunchKernelGGL(k_seg_fixup, gfix, bt, 0, stream, ta.segs, tails, ta.rt, hdr, in, out,
-                       status);
+  if (!DECRYPT) {
+    // companion: dense tile classes first, the long-latency tails last (they
+    // then overlap the segment kernel's drain; tails first: -3..5 %)
+    NOISE_DESC_TILES()
+    if ((e = hipStreamWaitEvent(ax.aux, ax.prep, 0)) != hipSuccess) return e;
+    hipLaunchKernelGGL((k_seg_tail<DECRYPT, kTailFused>), grid, bt, 0, ax.aux, tails, rt, hdr, in, out, -1);
+    if ((e = hipEventRecord(ax.join, ax.aux)) != hipSuccess) return e;
+    // caller: every full segment of every long record, then the tags
+    hipLaunchKernelGGL((k_aead_tile<DECRYPT, 1024, false, kTileSeg>), gseg, bt, 0, stream, a);
+    if ((e = hipStreamWaitEvent(stream, ax.join, 0)) != hipSuccess) return e;
+    hipLaunchKernelGGL((k_seg_finalize_w<DECRYPT, NOISE_FIN_W>), gfin, bt, 0, stream, fin, rt, ta.partial,
+                       ta.partial_hi, hdr_w, in, out, status, -1);
+    return hipGetLastError();
   }
+  // decrypt.  Companion: the tails' Poly1305 first (the first tag check
+  // waits for it), then the small classes and the generic kernel
+  if ((e = hipStreamWaitEvent(ax.aux, ax.prep, 0)) != hipSuccess) return e;
+  hipLaunchKernelGGL((k_seg_tail<true, kTailPoly>), grid, bt, 0, ax.aux, tails, rt, hdr, in, out, -1);
+  if ((e = hipEventRecord(ax.join, ax.aux)) != hipSuccess) return e;
+  NOISE_DESC_TILES()
+  // caller: the chunks' Poly1305 passes
+  TileArgs ac = a;
+  ac.seg_split = hdr->ssplit;
+  for (int c = 0; c < kSegChunks; ++c) {
+    ac.chunk = c;
+    hipLaunchKernelGGL((k_aead_tile<true, 1024, false, kTileSegPoly>), gseg, bt, 0, stream, ac);
+    if ((e = hipEventRecord(ax.poly[c], stream)) != hipSuccess) return e;
+  }
+  // companion 2: per chunk, the tag check, then the segments' plaintext; the
+  // companion writes the chunk's tails' plaintext beside it
+  if ((e = hipStreamWaitEvent(ax.aux2, ax.join, 0)) != hipSuccess) return e;  // tails' P_tail
+  for (int c = 0; c < kSegChunks; ++c) {
+    ac.chunk = c;
+    if ((e = hipStreamWaitEvent(ax.aux2, ax.poly[c], 0)) != hipSuccess) return e;
+    hipLaunchKernelGGL((k_seg_finalize_w<true, NOISE_FIN_W>), gfin, bt, 0, ax.aux2, fin, rt, ta.partial,
+                       ta.partial_hi, hdr_w, in, out, status, c);
+    if ((e = hipEventRecord(ax.fin[c], ax.aux2)) != hipSuccess) return e;
+    hipLaunchKernelGGL((k_aead_tile<true, 1024, false, kTileSegXor, 0, 1, NOISE_XOR_SPAN>), gseg, bt, 0,
+                       ax.aux2, ac);
+    if ((e = hipStreamWaitEvent(ax.aux, ax.fin[c], 0)) != hipSuccess) return e;
+    hipLaunchKernelGGL((k_seg_tail<true, kTailXor>), grid, bt, 0, ax.aux, tails, rt, hdr, in, out, c);
+  }
+#undef NOISE_DESC_TILE
+#undef NOISE_DESC_TILES
+  if ((e = hipEventRecord(ax.xdone, ax.aux2)) != hipSuccess) return e;
+  if ((e = hipEventRecord(ax.join2, ax.aux)) != hipSuccess) return e;
+  if ((e = hipStreamWaitEvent(stream, ax.xdone, 0)) != hipSuccess) return e;
+  if ((e = hipStreamWaitEvent(stream, ax.join2, 0)) != hipSuccess) return e;
   return hipGetLastError();
 }
 

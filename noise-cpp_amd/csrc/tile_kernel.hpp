@@ -75,7 +75,12 @@ enum TileMode : int {
   kTileSessions = 1,  // key row keys[key_idx[i]], nonce nonces[i], strided
   kTileDesc = 2,      // descriptor recs[idx[base + i]] (records API class)
   kTileSeg = 3,       // 1 KiB segment g of a long record (segs[g] -> SegRec):
-                      // ciphertext + Poly1305 partial sum, no tag
+                      // ciphertext + Poly1305 partial sum, no tag (encrypt)
+  kTileSegPoly = 4,   // decrypt pass 1: the segment's Poly1305 partial sum of
+                      // the ciphertext only (no keystream, nothing stored)
+  kTileSegXor = 5,    // decrypt pass 3 (after the tags are checked): keystream
+                      // XOR of the segments of VERIFIED records -> plaintext;
+                      // a failed record's segment: nothing (in place) / zeros
 };
 
 // ---- long records as 1 KiB segments (records_kernels.hip) -----------------
@@ -99,7 +104,8 @@ struct SegRec {                  // one per long record, 224 B
   uint32_t pw16[5], pw32[5], r64[5];      // r^16, r^32, r^64 (radix 2^26)
   uint32_t rtail[5];             // r^(tail blocks) (radix 2^26)
   uint32_t ptail[5];             // the tail's Poly1305 sum (radix 2^32, h4 small)
-  uint32_t pad[3];
+  uint32_t ok;                   // decrypt: 1 once the finalize kernel verified the tag
+  uint32_t pad[2];
 };
 static_assert(sizeof(SegRec) == 224, "SegRec layout");
 struct SegEntry {                // one per full segment
@@ -130,6 +136,8 @@ struct TileArgs {
   int cls;                       // kTileDesc: this launch's class
   const SegEntry *segs;          // kTileSeg
   const SegRec *rt;              // kTileSeg
+  const unsigned long long *seg_split;  // kTileSeg*: chunk boundaries (device), or null
+  int chunk;                     // kTileSeg*: this launch's chunk of seg_split
   SegPartial *partial;           // kTileSeg: P_s words 0..3
   uint32_t *partial_hi;          // kTileSeg: P_s word 4
   const unsigned long long *nseg;  // kTileSeg: number of segments (device)
@@ -141,8 +149,13 @@ template <int MODE>
 __device__ __forceinline__ void desc_class_range(const TileArgs &a,
                                                  uint64_t &base, uint64_t &n) {
   base = 0;
-  if (MODE == kTileSeg) {
+  if (MODE >= kTileSeg) {
     n = *a.nseg;
+    if (a.seg_split) {  // chunk c: [split[c], split[c + 1]), clamped to the segments there are
+      const uint64_t lo = a.seg_split[a.chunk], hi = a.seg_split[a.chunk + 1];
+      base = lo < n ? lo : n;
+      n = (hi < n ? hi : n) - base;
+    }
     return;
   }
   base = a.cls_base[a.cls];
@@ -158,7 +171,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
                                           uint32_t own_in_hi) {
   using C = TileCfg<L, SPAN>;
   if (ABL == 1) return;
-  constexpr bool TAGGED_IN = DECRYPT && MODE != kTileSeg;  // ct || tag pieces
+  constexpr bool TAGGED_IN = DECRYPT && MODE < kTileSeg;  // ct || tag pieces
   constexpr int IN_SLOTS = TAGGED_IN ? C::NSLOT : C::REC_SLOTS;
   if (CONTIG) {
     // slot s = 64q + lane holds piece swz(s) = 64q + gl[q & 3]; packed
@@ -192,7 +205,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
           lds_dma16_s(base, 16u * (r * (C::SPR + 1) + C::SPR), (lds_void *)(lds3 + 64 * q));
       }
     }
-  } else if (MODE == kTileSeg || (MODE == kTileDesc && C::SPR == 64)) {
+  } else if (MODE >= kTileSeg || (MODE == kTileDesc && C::SPR == 64)) {
     // 1 KiB units (segments, or kTileDesc records of exactly 1 KiB): DMA
     // instruction q moves all 64 pieces of unit q, so its offset is
     // wave-uniform -- read from the unit's key lane (v_readlane into SGPRs)
@@ -227,7 +240,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
         p = C::SPR;
       }
       const uint8_t *rec_base;
-      if (MODE == kTileDesc || MODE == kTileSeg) {  // offset of record r: key lane t*RPT + r
+      if (MODE == kTileDesc || MODE >= kTileSeg) {  // offset of record r: key lane t*RPT + r
         const uint32_t src = t_rpt + (r < (uint32_t)C::RPT ? r : 0u);
         const uint64_t off = ((uint64_t)(uint32_t)__shfl((int)own_in_hi, src) << 32) |
                              (uint32_t)__shfl((int)own_in_lo, src);
@@ -250,41 +263,56 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
 // kTileSeg (L = 1024): unit i is full segment i of a long record (SegEntry ->
 // SegRec): no key block (r and its powers come from the SegRec), ChaCha
 // counters 1 + 16 s + ..., no tag: the segment's Poly1305 partial sum goes to
-// a.partial[i].  Decrypt writes the plaintext unconditionally (the finalize
-// and fix-up kernels restore or zero the record if its tag fails).
+// a.partial[i] (encrypt).  Decrypt splits the same unit into kTileSegPoly
+// (the partial sum of the ciphertext, nothing stored) and, after the tags are
+// checked, kTileSegXor (plaintext of the verified records only).  With
+// a.seg_split set, a launch covers the segments [split[c], split[c + 1]) of
+// chunk c = a.chunk only (records_kernels.hip: the decrypt pipeline).
 // ABL (ablation, tools/ubench only; the product uses 0): 1 = no HBM traffic
 // (compute on whatever the LDS holds), 2 = no Poly1305 work.
 // NBUF = 2: two LDS tile buffers -- tile t+1's DMA is issued before tile t's
 // compute (instead of after it), so it lands during the compute; the wave
 // then waits only for it (a counted vmcnt lets tile t-1's stores stay in
 // flight).  Twice the LDS: 33 KB per wave at L = 1024, one wave per SIMD.
-// kTileSeg: the per-lane metadata of one segment (from its SegRec)
+// kTileSeg*: the per-lane metadata of one segment (from its SegRec); each
+// pass loads only what it uses (the Poly1305 pass no key, the XOR pass no r)
 struct SegMeta {
   uint32_t k[8], r[4], pw16[5], pw32[5];
-  uint32_t nlo, nhi, in_lo, in_hi, out_lo, out_hi, cb;
+  uint32_t nlo, nhi, in_lo, in_hi, out_lo, out_hi, cb, ok, inpl;
 };
+template <int MODE>
 __device__ __forceinline__ void seg_meta_load(SegMeta &m, const SegRec *rt, const SegEntry e,
-                                              bool valid) {
+                                              bool valid, const uint8_t *in, const uint8_t *out) {
+  constexpr bool XOR = MODE != kTileSegPoly, POLY = MODE != kTileSegXor;
 #pragma unroll
   for (int i = 0; i < 8; ++i) m.k[i] = 0u;
 #pragma unroll
   for (int i = 0; i < 4; ++i) m.r[i] = 0u;
 #pragma unroll
   for (int i = 0; i < 5; ++i) m.pw16[i] = m.pw32[i] = i == 0 ? 1u : 0u;
-  m.nlo = m.nhi = m.in_lo = m.in_hi = m.out_lo = m.out_hi = m.cb = 0u;
+  m.nlo = m.nhi = m.in_lo = m.in_hi = m.out_lo = m.out_hi = m.cb = m.ok = m.inpl = 0u;
   if (valid) {
     const SegRec &R = rt[e.q];
     const uint64_t io = R.in_off + 1024ull * e.s, oo = R.out_off + 1024ull * e.s;
     m.in_lo = (uint32_t)io; m.in_hi = (uint32_t)(io >> 32);
     m.out_lo = (uint32_t)oo; m.out_hi = (uint32_t)(oo >> 32);
-    m.nlo = (uint32_t)R.nonce; m.nhi = (uint32_t)(R.nonce >> 32);
-    m.cb = 16u * e.s;
+    if (XOR) {
+      m.nlo = (uint32_t)R.nonce; m.nhi = (uint32_t)(R.nonce >> 32);
+      m.cb = 16u * e.s;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) m.k[i] = R.k[i];
+      for (int i = 0; i < 8; ++i) m.k[i] = R.k[i];
+    }
+    if (POLY) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) m.r[i] = R.r[i];
+      for (int i = 0; i < 4; ++i) m.r[i] = R.r[i];
 #pragma unroll
-    for (int i = 0; i < 5; ++i) { m.pw16[i] = R.pw16[i]; m.pw32[i] = R.pw32[i]; }
+      for (int i = 0; i < 5; ++i) { m.pw16[i] = R.pw16[i]; m.pw32[i] = R.pw32[i]; }
+    }
+    if (MODE == kTileSegXor) {
+      m.ok = R.ok;
+      m.inpl = in + R.in_off == out + R.out_off;
+    }
+
   }
 }
 
@@ -293,7 +321,10 @@ template <bool DECRYPT, int L, bool CONTIG, int MODE = kTileUniform, int ABL = 0
 __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
   using C = TileCfg<L, SPAN>;
   constexpr bool KEYED = MODE != kTileUniform;
-  constexpr bool SEG = MODE == kTileSeg;
+  constexpr bool SEG = MODE >= kTileSeg;              // segments of long records
+  constexpr bool DO_POLY = MODE != kTileSegXor;       // Poly1305 over the ciphertext
+  constexpr bool DO_XOR = MODE != kTileSegPoly;       // keystream XOR + stores
+  static_assert(MODE < kTileSegPoly || DECRYPT, "the split segment passes are decrypt's");
   constexpr int OPR = (DECRYPT || SEG) ? C::SPR : C::SPR + 1;  // out pieces / record
   constexpr int OUT_SLOTS = C::RPT * OPR;
   // RECW (contiguous encrypt of records of >= 1 KiB): output instruction
@@ -310,7 +341,8 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
   constexpr int NDATA = C::RPT * C::SPR / 64;
   constexpr int NOUT = RECW ? NDATA + 1 : (OUT_SLOTS + 63) / 64;  // store instructions
   static_assert(!(CONTIG && (MODE == kTileDesc || SEG)), "descriptor tiles are strided");
-  static_assert(!SEG || (L == 1024 && SPAN == 256), "segments are 1 KiB, 256 B per lane");
+  static_assert(!SEG || (L == 1024 && (SPAN == 256 || (SPAN == 128 && !DO_POLY))),
+                "segments are 1 KiB, 256 B per lane (128 B: the XOR pass, which needs no r powers)");
   static_assert(NBUF == 1 || NBUF == 2, "one or two tile buffers");
   __shared__ uint4 lds[NBUF * C::NSLOT];
   const uint32_t lane = threadIdx.x;
@@ -337,8 +369,8 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
   SegEntry nxt_e{0u, 0u};
   if (SEG) {
     const uint64_t g = (uint64_t)blockIdx.x * 64 + lane;
-    if (g < nrec) nxt_e = a.segs[g];
-    seg_meta_load(nxt, a.rt, nxt_e, g < nrec);
+    if (g < nrec) nxt_e = a.segs[dbase + g];
+    seg_meta_load<MODE>(nxt, a.rt, nxt_e, g < nrec, in, out);
   }
 
 #pragma unroll 1
@@ -351,6 +383,10 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
   uint32_t own_in_lo = 0, own_in_hi = 0, own_out_lo = 0, own_out_hi = 0, own_di = 0;
   uint32_t own_cb = 0;  // kTileSeg: first ChaCha block counter - 1 (16 s)
   bool own_bad = false, own_inplace = false;
+  uint32_t own_ok = 1u;  // kTileSegXor: the record's tag verified
+  // kTileSegXor: per super-tile, bit l = segment super0 + l's record failed /
+  // is decrypted in place (ballots of the lanes' own metadata: no shuffles)
+  uint64_t seg_nok = 0, seg_inpl = 0;
   const uint64_t next0 = super0 + (uint64_t)gridDim.x * 64;  // kTileSeg prefetch
   if (SEG) {
 #pragma unroll
@@ -364,13 +400,20 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     own_in_lo = nxt.in_lo; own_in_hi = nxt.in_hi;
     own_out_lo = nxt.out_lo; own_out_hi = nxt.out_hi;
     own_cb = nxt.cb;
+    own_ok = nxt.ok;
+    own_inplace = nxt.inpl != 0u;
+    if (MODE == kTileSegXor) {  // lane l <-> segment super0 + l: wave-uniform masks
+      seg_nok = __ballot(own_ok == 0u);
+      seg_inpl = __ballot(own_inplace);
+    }
+
     const uint64_t left = nrec - super0;
     tile_load<L, DECRYPT, CONTIG, MODE, ABL, SPAN>(
         NOISE_LDS3(lds), in, a.in_stride, super0,
         left < (uint64_t)C::RPT ? (uint32_t)left : C::RPT, lane, gl, 0u,
         own_in_lo, own_in_hi);
     nxt_e = SegEntry{0u, 0u};
-    if (next0 + lane < nrec) nxt_e = a.segs[next0 + lane];
+    if (next0 + lane < nrec) nxt_e = a.segs[dbase + next0 + lane];
   } else {
     uint64_t n = a.nonce0 + super0 + lane;
     if (KEYED) {
@@ -448,7 +491,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     if (NBUF == 2 && prev_all) wait_vmcnt<NOUT>();
     else wait_vmem();
     wave_lds_fence();
-    if (SEG && t == 0) seg_meta_load(nxt, a.rt, nxt_e, next0 + lane < nrec);
+    if (SEG && t == 0) seg_meta_load<MODE>(nxt, a.rt, nxt_e, next0 + lane < nrec, in, out);
     if (NBUF == 2 && t + 1 < C::G) {  // the next tile's DMA now, into the other buffer
       const uint64_t nrec0 = rec0 + C::RPT;
       if (nrec0 < nrec) {
@@ -463,64 +506,74 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     // ---- per-lane record work -------------------------------------------
     const uint32_t src = (uint32_t)t * C::RPT + rho;  // key lane of my record
     Poly1305 p;
-    p.r0 = __shfl(kr[0], src); p.r1 = __shfl(kr[1], src);
-    p.r2 = __shfl(kr[2], src); p.r3 = __shfl(kr[3], src);
-    p.rr0 = (p.r0 >> 2) * 5u;
-    p.rr1 = p.r1 + (p.r1 >> 2);
-    p.rr2 = p.r2 + (p.r2 >> 2);
-    p.rr3 = p.r3 + (p.r3 >> 2);
-    p.r0lo = p.r0 & 3u;
-    p.s0 = __shfl(kss[0], src); p.s1 = __shfl(kss[1], src);
-    p.s2 = __shfl(kss[2], src); p.s3 = __shfl(kss[3], src);
     p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0;
+    if (DO_POLY) {
+      p.r0 = __shfl(kr[0], src); p.r1 = __shfl(kr[1], src);
+      p.r2 = __shfl(kr[2], src); p.r3 = __shfl(kr[3], src);
+      p.rr0 = (p.r0 >> 2) * 5u;
+      p.rr1 = p.r1 + (p.r1 >> 2);
+      p.rr2 = p.r2 + (p.r2 >> 2);
+      p.rr3 = p.r3 + (p.r3 >> 2);
+      p.r0lo = p.r0 & 3u;
+      p.s0 = __shfl(kss[0], src); p.s1 = __shfl(kss[1], src);
+      p.s2 = __shfl(kss[2], src); p.s3 = __shfl(kss[3], src);
+    }
 
     uint32_t n_lo, n_hi;
     bool bad_key = false;
     uint32_t kt[8];  // this record's key
 #pragma unroll
-    for (int i = 0; i < 8; ++i) kt[i] = KEYED ? __shfl(own_k[i], src) : k[i];
-    if (KEYED) {
+    for (int i = 0; i < 8; ++i) kt[i] = !DO_XOR ? 0u : KEYED ? __shfl(own_k[i], src) : k[i];
+    if (KEYED && DO_XOR) {
       n_lo = __shfl(own_nlo, src);
       n_hi = __shfl(own_nhi, src);
       bad_key = __shfl((int)own_bad, src) != 0;
-    } else {
+    } else if (!KEYED) {
       const uint64_t n = a.nonce0 + rec0 + rho;
       n_lo = (uint32_t)n;
       n_hi = (uint32_t)(n >> 32);
+    } else {  // kTileSegPoly: no keystream
+      n_lo = n_hi = 0u;
     }
     // Software pipeline: the ChaCha block of chunk kk+1 is independent of
     // the (serial) Poly1305 chain of chunk kk, so both sit in one basic
     // block and the scheduler interleaves them.
     const uint32_t c0 = j * C::CPL;  // first 64-B chunk of my span (in the record / segment)
-    const uint32_t cb = 1u + c0 + (SEG ? (uint32_t)__shfl((int)own_cb, src) : 0u);  // its counter
-    const ChaPre pre = chacha_pre(kt, n_lo, n_hi);
+    const uint32_t cb = 1u + c0 + (SEG && DO_XOR ? (uint32_t)__shfl((int)own_cb, src) : 0u);  // its counter
+    ChaPre pre{};
     uint32_t ks[16];
-    chacha20_block_pre(kt, cb, pre, n_lo, n_hi, ks);
+    if (DO_XOR) {
+      pre = chacha_pre(kt, n_lo, n_hi);
+      chacha20_block_pre(kt, cb, pre, n_lo, n_hi, ks);
+    }
 #pragma unroll
     for (int kk = 0; kk < C::CPL; ++kk) {
       const uint32_t c = c0 + kk;
       uint32_t ksn[16];
-      if (kk + 1 < C::CPL) chacha20_block_pre(kt, cb + 1u + kk, pre, n_lo, n_hi, ksn);
+      if (DO_XOR && kk + 1 < C::CPL) chacha20_block_pre(kt, cb + 1u + kk, pre, n_lo, n_hi, ksn);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint32_t slot = swz(rho * C::SPR + 4u * c + q);
         const uint4 v = lb[slot];
-        uint4 o;
-        o.x = v.x ^ ks[4 * q + 0];
-        o.y = v.y ^ ks[4 * q + 1];
-        o.z = v.z ^ ks[4 * q + 2];
-        o.w = v.w ^ ks[4 * q + 3];
-        lb[slot] = o;
-        if (ABL == 2) { p.h0 ^= o.x ^ v.y; p.h1 ^= o.z ^ v.w; }
+        uint4 o = v;
+        if (DO_XOR) {
+          o.x = v.x ^ ks[4 * q + 0];
+          o.y = v.y ^ ks[4 * q + 1];
+          o.z = v.z ^ ks[4 * q + 2];
+          o.w = v.w ^ ks[4 * q + 3];
+          lb[slot] = o;
+        }
+        if (!DO_POLY) {
+        } else if (ABL == 2) { p.h0 ^= o.x ^ v.y; p.h1 ^= o.z ^ v.w; }
         else if (DECRYPT) poly_block(p, v.x, v.y, v.z, v.w);
         else poly_block(p, o.x, o.y, o.z, o.w);
       }
-      if (kk + 1 < C::CPL) {
+      if (DO_XOR && kk + 1 < C::CPL) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) ks[i] = ksn[i];
       }
     }
-    if (C::G > 1) {
+    if (C::G > 1 && DO_POLY) {
       // acc_j * r^(BPL (G-1-j)), then sum over the record's G lanes
       F26 h = to26(p.h0, p.h1, p.h2, p.h3, p.h4);
       const uint32_t m = C::G - 1 - j;
@@ -552,9 +605,9 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     if (SEG) {
       // the segment's partial sum (no length block, no s); lane 0 of the
       // segment stores it
-      if (j == 0 && valid) {
+      if (DO_POLY && j == 0 && valid) {
         const u32x4 w0 = {p.h0, p.h1, p.h2, p.h3};
-        const uint64_t g = super0 + (uint64_t)t * C::RPT + rho;
+        const uint64_t g = dbase + super0 + (uint64_t)t * C::RPT + rho;
         __builtin_nontemporal_store(w0, (g_u32x4 *)(a.partial + g));
         __builtin_nontemporal_store(p.h4, (__attribute__((address_space(1))) uint32_t *)(a.partial_hi + g));
       }
@@ -568,8 +621,19 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     // cross-lane reads stay outside divergent code: a ds_bpermute from a lane
     // that is inactive does not return that lane's value
     const uint32_t rec_di = MODE == kTileDesc ? (uint32_t)__shfl((int)own_di, src) : 0u;
+    constexpr bool PER_REC_INPL = MODE == kTileDesc || MODE == kTileSegXor;
     const bool rec_inplace = MODE == kTileDesc ? __shfl((int)own_inplace, src) != 0 : false;
-    if (SEG) {
+    uint64_t inpl_seg = 0;  // kTileSegXor: bit r * G = slot r is in place
+    if (MODE == kTileSegXor) {
+      // a segment of a record whose tag failed: not output as computed.  Slot
+      // r of tile t is segment super0 + t RPT + r: bit t RPT + r of the masks
+      const uint32_t nok = (uint32_t)(seg_nok >> (t * C::RPT)), ip = (uint32_t)(seg_inpl >> (t * C::RPT));
+#pragma unroll
+      for (int r = 0; r < C::RPT; ++r) {
+        fail_mask |= (uint64_t)((nok >> r) & 1u) << (r * C::G);
+        inpl_seg |= (uint64_t)((ip >> r) & 1u) << (r * C::G);
+      }
+    } else if (SEG) {
     } else if (DECRYPT) {
       const uint4 want = lb[C::REC_SLOTS + rho];
       const uint32_t diff = (want.x ^ tag[0]) | (want.y ^ tag[1]) |
@@ -582,9 +646,27 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     } else if (j == 0) {
       lb[C::REC_SLOTS + rho] = make_uint4(tag[0], tag[1], tag[2], tag[3]);
     }
-    // kTileDesc: a failed in-place record is kept, a failed copy is zeroed
-    const uint64_t inpl_mask = MODE == kTileDesc ? __ballot(j == 0 && rec_inplace) : 0ull;
+    // kTileDesc / kTileSegXor: a failed in-place record is kept, a failed
+    // copy is zeroed
+    const uint64_t inpl_mask = MODE == kTileSegXor ? inpl_seg
+                               : PER_REC_INPL ? __ballot(j == 0 && rec_inplace) : 0ull;
     wave_lds_fence();
+    if (!DO_XOR) {  // kTileSegPoly: nothing to store; the next tile's DMA
+      prev_all = false;
+      if (t + 1 < C::G) {
+        const uint64_t nrec0 = rec0 + C::RPT;
+        if (nrec0 < nrec) {
+          wait_lds();  // this tile's LDS reads done before the DMA overwrites them
+          wave_lds_fence();
+          const uint64_t left = nrec - nrec0;
+          tile_load<L, DECRYPT, CONTIG, MODE, ABL, SPAN>(
+              NOISE_LDS3(lds), in, a.in_stride, nrec0,
+              left < (uint64_t)C::RPT ? (uint32_t)left : C::RPT, lane, gl,
+              (uint32_t)(t + 1) * C::RPT, own_in_lo, own_in_hi);
+        }
+      }
+      continue;
+    }
 
     // ---- gather this tile's output records into registers, store them --
     // Keyed modes gather and store in NPART parts: 17 uint4 pieces live at
@@ -599,7 +681,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     // destination, v_readlane), instruction RPT (encrypt) the RPT tags
     constexpr bool RECQ = SEG || (MODE == kTileDesc && C::SPR == 64);
     auto piece = [&](int q, uint32_t &r, uint32_t &pc, uint32_t &slot, bool &ok) {
-      if (RECW) {
+      if constexpr (RECW) {
         if (q < NDATA) {
           r = (uint32_t)q / (C::SPR / 64);
           pc = 64u * ((uint32_t)q % (C::SPR / 64)) + lane;
@@ -658,8 +740,8 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
           piece(q, r, pc, slot, ok);
           if ((fail_mask >> (r * C::G)) & 1u) {
             const bool bad_key_rec = KEYED && ((badk_mask >> (r * C::G)) & 1u);
-            const bool inpl = MODE == kTileDesc ? ((inpl_mask >> (r * C::G)) & 1u) != 0
-                                                : a.in_place != 0;
+            const bool inpl = PER_REC_INPL ? ((inpl_mask >> (r * C::G)) & 1u) != 0
+                                           : a.in_place != 0;
             st[qq] = st[qq] && DECRYPT && !inpl && !bad_key_rec;
             ov[qq] = make_uint4(0u, 0u, 0u, 0u);
           }

@@ -20,6 +20,10 @@
 namespace noise_amd {
 
 inline bool dev_pools(int dev) {
+#if defined(NOISE_NO_MEMPOOL)
+  (void)dev;
+  return false;
+#endif
   constexpr int kMaxDev = 64;
   static std::atomic<int> known[kMaxDev];  // 0 unknown, 1 pools, 2 none
   if (dev < 0 || dev >= kMaxDev) return false;

@@ -52,9 +52,17 @@ def _run(binary, mode, nrec, seed, gap):
     ("ragged", 300, 6, 0),
 ])
 def test_records_path_emulated(emu_bin, mode, nrec, seed, gap):
+    """...and verify-before-write (crypto_aead_read, monocypher.c:2912-2929):
+    every 16-byte store of the decrypt is watched (tools/emu store hook); no
+    store puts a non-zero byte into the output range of a record whose tag
+    fails, nor lands at all in one decrypted in place -- the segmented path
+    (>= 1 KiB records) included: its Poly1305 pass and the finalize check
+    every tag before the keystream pass writes any plaintext."""
     r = _run(emu_bin, mode, nrec, seed, gap)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]
     assert "ok (0 failures)" in r.stdout
+    assert ": 0 stores of unverified plaintext" in r.stdout
+    assert "watched 0 failed" not in r.stdout  # the batch holds tampered long records
 
 
 def test_host_entry_points_emulated_and_wiped():

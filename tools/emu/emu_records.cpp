@@ -13,6 +13,8 @@
 //   emu_records <mode> <nrec> <seed> <gap>: records start <gap> bytes into
 //     each buffer (e.g. 4 GiB, to exercise 64-bit offsets)
 // Test infrastructure only (links oracle/chachapoly_oracle.c).
+#include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -31,6 +33,43 @@ static uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
   z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
   return z ^ (z >> 31);
+}
+
+// Decrypt with the store hook on: no store may put a non-zero byte into the
+// output range of a record whose tag fails, nor any store at all into one
+// decrypted in place (crypto_aead_read, monocypher.c:2912-2929: plaintext is
+// written only after the tag has verified).  Ranges sorted by start.
+struct Range {
+  uintptr_t lo, hi;
+};
+static std::vector<Range> g_bad_ranges;
+static bool g_bad_in_place = false;
+static std::atomic<long> g_bad_stores{0}, g_bad_first{-1};
+static uintptr_t g_out_lo = 0, g_out_hi = 0;  // the decrypt's output buffer
+static std::atomic<long> g_out_of_range{0};
+static void watch_store(const void *dst, const void *data, int n) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(dst), b = a + (uintptr_t)n;
+  if (a < g_out_lo || b > g_out_hi) {  // reported, and not performed by ASan either
+    if (g_out_of_range.fetch_add(1) < 5)
+      std::printf("store outside the output buffer: offset %lld, %d bytes\n",
+                  (long long)(a - g_out_lo), n);
+    std::fflush(stdout);
+    std::abort();
+  }
+  auto it = std::upper_bound(g_bad_ranges.begin(), g_bad_ranges.end(), a,
+                             [](uintptr_t x, const Range &r) { return x < r.lo; });
+  // the range starting at or before a, and the next one (a store may straddle)
+  for (int k = 0; k < 2; ++k) {
+    const Range *r = nullptr;
+    if (k == 0 && it != g_bad_ranges.begin()) r = &*(it - 1);
+    if (k == 1 && it != g_bad_ranges.end()) r = &*it;
+    if (!r || b <= r->lo || a >= r->hi) continue;
+    bool bad = g_bad_in_place;
+    const uint8_t *p = static_cast<const uint8_t *>(data);
+    for (int i = 0; i < n && !bad; ++i)
+      if (a + (uintptr_t)i >= r->lo && a + (uintptr_t)i < r->hi && p[i] != 0) bad = true;
+    if (bad && g_bad_stores.fetch_add(1) == 0) g_bad_first = (long)(a - r->lo);
+  }
 }
 
 static int fails = 0;
@@ -118,8 +157,22 @@ int main(int argc, char **argv) {
   if (!in_place) std::memset(back + gap, 0xC3, tot_in - gap);
   uint8_t *st = (uint8_t *)std::malloc(R);
   std::memset(st, 9, R);
+  for (uint64_t i = 0; i < R; ++i)
+    if (bad[i])
+      g_bad_ranges.push_back(Range{reinterpret_cast<uintptr_t>(back + dec[i].out_off),
+                                   reinterpret_cast<uintptr_t>(back + dec[i].out_off) + lens[i]});
+  std::sort(g_bad_ranges.begin(), g_bad_ranges.end(), [](const Range &x, const Range &y) { return x.lo < y.lo; });
+  g_bad_in_place = in_place;
+  g_out_lo = reinterpret_cast<uintptr_t>(back);
+  g_out_hi = g_out_lo + tot_in;
+  emu::store_hook = watch_store;
   e = noise_amd::launch_aead_records(true, d_key, 1, d_dec, R, ct, back, nullptr, st, nullptr);
+  emu::store_hook = nullptr;
   CHECK(e == hipSuccess, "decrypt launch %d", e);
+  CHECK(g_bad_stores.load() == 0, "%ld stores of unverified plaintext into failed records (first at byte %ld)",
+        g_bad_stores.load(), g_bad_first.load());
+  std::printf("watched %zu failed records: %ld stores of unverified plaintext\n", g_bad_ranges.size(),
+              g_bad_stores.load());
   for (uint64_t i = 0; i < R; ++i) {
     const uint32_t L = lens[i];
     if (bad[i]) {

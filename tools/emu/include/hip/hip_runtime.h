@@ -89,6 +89,11 @@ inline std::atomic<int> async_running{0};
 inline std::mutex async_mu;
 inline std::vector<std::thread> async_threads;
 
+// called by store16 (chachapoly_device.hpp) before every 16-byte record
+// store -- ciphertext, plaintext, tags, zero fills -- with the destination,
+// the data and its byte count: a test can watch what lands where
+inline void (*store_hook)(const void *dst, const void *data, int n) = nullptr;
+
 // every hipMalloc / hipHostMalloc allocation, for tests that inspect what
 // the engine leaves in its buffers (secret hygiene)
 struct Alloc {

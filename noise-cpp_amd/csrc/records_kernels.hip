@@ -52,7 +52,7 @@ constexpr int kCols = kNumCls + 2 + kFinBuckets;
 // Decrypt pipelines the long records in kSegChunks chunks (launch_classes):
 // the Poly1305 pass of chunk c + 1 (HBM-bound) runs beside the keystream pass
 // of chunk c (VALU-bound).  Chunk boundaries fall on record starts, near
-// c * nseg / kSegChunks segments.
+// (2c - 1) nseg / (2 kSegChunks - 1) segments (chunk 0 half the others).
 #ifndef NOISE_SEG_CHUNKS
 #define NOISE_SEG_CHUNKS 4
 #endif
@@ -67,6 +67,10 @@ constexpr int kSegChunks = NOISE_SEG_CHUNKS;
 // 3.54-3.61 ms per decrypt against 3.83-3.90 at 256 B.
 #ifndef NOISE_XOR_SPAN
 #define NOISE_XOR_SPAN 128
+#endif
+// The Poly1305 pass's span per lane (r^8 from the SegRec at 128 B)
+#ifndef NOISE_POLY_SPAN
+#define NOISE_POLY_SPAN 128
 #endif
 #ifndef NOISE_CLASSIFY_MIN  // overridable for the CPU emulation build
 #define NOISE_CLASSIFY_MIN 2048
@@ -356,7 +360,9 @@ __global__ __launch_bounds__(64) void k_cls_scatter(
       const unsigned long long total = hdr->counts[kColSegs];
 #pragma unroll
       for (int k = 1; k < kSegChunks; ++k) {  // the record holding a chunk's first segment
-        const unsigned long long b = total * (unsigned long long)k / kSegChunks;
+        // chunk 0 half the size of the others (1 : 2 : 2 : ...): the first
+        // tag check, and so the keystream pass, can start sooner
+        const unsigned long long b = total * (2ull * k - 1ull) / (2ull * kSegChunks - 1ull);
         if (seg0 <= b && b < seg0 + nf) {
           hdr->qsplit[k] = q;
           hdr->ssplit[k] = seg0;
@@ -413,13 +419,14 @@ __global__ __launch_bounds__(64) void k_seg_prep(const uint8_t *__restrict__ key
     // squaring chain r^(2^b); r^(tail blocks) = product over the bits of
     // the tail's Poly1305 block count (1..64)
     const uint32_t nbt = ((R.len & 1023u) + 15u) >> 4;
-    F26 x = to26(r0, r1, r2, r3, 0u), rt_pow;
+    F26 x = to26(r0, r1, r2, r3, 0u), rt_pow, x8;
     rt_pow.a[0] = 1u;
     rt_pow.a[1] = rt_pow.a[2] = rt_pow.a[3] = rt_pow.a[4] = 0u;
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       if ((nbt >> b) & 1u) rt_pow = mul26(rt_pow, x);
       x = mul26(x, x);
+      if (b == 2) x8 = x;  // r^8
     }
     // x = r^16
     if ((nbt >> 4) & 1u) rt_pow = mul26(rt_pow, x);
@@ -428,6 +435,7 @@ __global__ __launch_bounds__(64) void k_seg_prep(const uint8_t *__restrict__ key
     if ((nbt >> 6) & 1u) rt_pow = mul26(rt_pow, x64);  // a 1009..1023-byte tail: 64 blocks
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
+      R.pw8[i] = x8.a[i];
       R.pw16[i] = x.a[i];
       R.pw32[i] = x32.a[i];
       R.r64[i] = x64.a[i];
@@ -910,11 +918,11 @@ static hipError_t aux_release(int dev, hipStream_t stream) {
 // the keystream pass VALU-bound, so the long records go through in
 // kSegChunks chunks and the Poly1305 pass of chunk c + 1 runs beside the
 // tag check and keystream pass of chunk c:
-//   caller     : prep -> Poly(0) -> Poly(1) -> ... -> Poly(K-1)           (wait xdone, join2)
-//   companion  : (fork) small classes, generic, (wait prep) tail Poly1305 -> join
-//                                     ... (wait fin) tail plaintext -> join2
-//   companion 2: (wait join) (wait poly[c]) finalize(c) -> XOR(c), c = 0 .. K-1;
-//                fin after finalize(K-1), xdone after XOR(K-1)
+//   caller     : prep -> Poly(0) -(wait join)-> check(0) -> Poly(1) -> check(1) -> ...
+//                ... -> check(K-1)                                   (wait xdone, join2)
+//   companion  : (wait prep) tail Poly1305 -> join, small classes, generic,
+//                then per chunk (wait fin[c]) the chunk's tail plaintext -> join2
+//   companion 2: per chunk (wait fin[c]) XOR(c) -> xdone
 template <bool DECRYPT>
 static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr *hdr,
                                  const uint8_t *keys, uint32_t nkeys,
@@ -977,23 +985,26 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   hipLaunchKernelGGL((k_seg_tail<true, kTailPoly>), grid, bt, 0, ax.aux, tails, rt, hdr, in, out, -1);
   if ((e = hipEventRecord(ax.join, ax.aux)) != hipSuccess) return e;
   NOISE_DESC_TILES()
-  // caller: the chunks' Poly1305 passes
+  // caller: per chunk, the Poly1305 pass and the tag check (the first one
+  // also waits for the tails' P_tail).  The checks sit here, not in front of
+  // the keystream passes, so chunk c + 1's is done while chunk c's plaintext
+  // is being written and the keystream passes follow each other without gaps
   TileArgs ac = a;
   ac.seg_split = hdr->ssplit;
   for (int c = 0; c < kSegChunks; ++c) {
     ac.chunk = c;
-    hipLaunchKernelGGL((k_aead_tile<true, 1024, false, kTileSegPoly>), gseg, bt, 0, stream, ac);
-    if ((e = hipEventRecord(ax.poly[c], stream)) != hipSuccess) return e;
+    hipLaunchKernelGGL((k_aead_tile<true, 1024, false, kTileSegPoly, 0, 1, NOISE_POLY_SPAN>), gseg, bt, 0,
+                       stream, ac);
+    if (c == 0 && (e = hipStreamWaitEvent(stream, ax.join, 0)) != hipSuccess) return e;
+    hipLaunchKernelGGL((k_seg_finalize_w<true, NOISE_FIN_W>), gfin, bt, 0, stream, fin, rt, ta.partial,
+                       ta.partial_hi, hdr_w, in, out, status, c);
+    if ((e = hipEventRecord(ax.fin[c], stream)) != hipSuccess) return e;
   }
-  // companion 2: per chunk, the tag check, then the segments' plaintext; the
-  // companion writes the chunk's tails' plaintext beside it
-  if ((e = hipStreamWaitEvent(ax.aux2, ax.join, 0)) != hipSuccess) return e;  // tails' P_tail
+  // companion 2: the segments' plaintext, chunk by chunk; the companion
+  // writes each chunk's tails' plaintext beside it
   for (int c = 0; c < kSegChunks; ++c) {
     ac.chunk = c;
-    if ((e = hipStreamWaitEvent(ax.aux2, ax.poly[c], 0)) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_seg_finalize_w<true, NOISE_FIN_W>), gfin, bt, 0, ax.aux2, fin, rt, ta.partial,
-                       ta.partial_hi, hdr_w, in, out, status, c);
-    if ((e = hipEventRecord(ax.fin[c], ax.aux2)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(ax.aux2, ax.fin[c], 0)) != hipSuccess) return e;
     hipLaunchKernelGGL((k_aead_tile<true, 1024, false, kTileSegXor, 0, 1, NOISE_XOR_SPAN>), gseg, bt, 0,
                        ax.aux2, ac);
     if ((e = hipStreamWaitEvent(ax.aux, ax.fin[c], 0)) != hipSuccess) return e;

@@ -95,7 +95,7 @@ enum TileMode : int {
 // (Horner in R = r^64), appends the tail (k_seg_tail: the len % 1024 bytes
 // past the last full segment, one lane per tail) as h r^(tail blocks) +
 // P_tail, then the length block and the tag.
-struct SegRec {                  // one per long record, 224 B
+struct SegRec {                  // one per long record, 256 B (two 128-B lines)
   uint64_t in_off, out_off, nonce, seg0;  // seg0: index of segment 0
   uint32_t k[8];                 // the record's key (copied from the key table)
   uint32_t key_idx, di, len, nfull;       // di: descriptor index
@@ -105,9 +105,10 @@ struct SegRec {                  // one per long record, 224 B
   uint32_t rtail[5];             // r^(tail blocks) (radix 2^26)
   uint32_t ptail[5];             // the tail's Poly1305 sum (radix 2^32, h4 small)
   uint32_t ok;                   // decrypt: 1 once the finalize kernel verified the tag
-  uint32_t pad[2];
+  uint32_t pw8[5];               // r^8 (radix 2^26): the 128-B span passes
+  uint32_t pad[5];
 };
-static_assert(sizeof(SegRec) == 224, "SegRec layout");
+static_assert(sizeof(SegRec) == 256, "SegRec layout");
 struct SegEntry {                // one per full segment
   uint32_t q, s;                 // long-record index, segment number
 };
@@ -277,10 +278,10 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
 // kTileSeg*: the per-lane metadata of one segment (from its SegRec); each
 // pass loads only what it uses (the Poly1305 pass no key, the XOR pass no r)
 struct SegMeta {
-  uint32_t k[8], r[4], pw16[5], pw32[5];
+  uint32_t k[8], r[4], pw8[5], pw16[5], pw32[5];
   uint32_t nlo, nhi, in_lo, in_hi, out_lo, out_hi, cb, ok, inpl;
 };
-template <int MODE>
+template <int MODE, int SPAN>
 __device__ __forceinline__ void seg_meta_load(SegMeta &m, const SegRec *rt, const SegEntry e,
                                               bool valid, const uint8_t *in, const uint8_t *out) {
   constexpr bool XOR = MODE != kTileSegPoly, POLY = MODE != kTileSegXor;
@@ -289,7 +290,7 @@ __device__ __forceinline__ void seg_meta_load(SegMeta &m, const SegRec *rt, cons
 #pragma unroll
   for (int i = 0; i < 4; ++i) m.r[i] = 0u;
 #pragma unroll
-  for (int i = 0; i < 5; ++i) m.pw16[i] = m.pw32[i] = i == 0 ? 1u : 0u;
+  for (int i = 0; i < 5; ++i) m.pw8[i] = m.pw16[i] = m.pw32[i] = i == 0 ? 1u : 0u;
   m.nlo = m.nhi = m.in_lo = m.in_hi = m.out_lo = m.out_hi = m.cb = m.ok = m.inpl = 0u;
   if (valid) {
     const SegRec &R = rt[e.q];
@@ -306,7 +307,11 @@ __device__ __forceinline__ void seg_meta_load(SegMeta &m, const SegRec *rt, cons
 #pragma unroll
       for (int i = 0; i < 4; ++i) m.r[i] = R.r[i];
 #pragma unroll
-      for (int i = 0; i < 5; ++i) { m.pw16[i] = R.pw16[i]; m.pw32[i] = R.pw32[i]; }
+      for (int i = 0; i < 5; ++i) {
+        if (SPAN == 128) m.pw8[i] = R.pw8[i];
+        m.pw16[i] = R.pw16[i];
+        m.pw32[i] = R.pw32[i];
+      }
     }
     if (MODE == kTileSegXor) {
       m.ok = R.ok;
@@ -341,8 +346,8 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
   constexpr int NDATA = C::RPT * C::SPR / 64;
   constexpr int NOUT = RECW ? NDATA + 1 : (OUT_SLOTS + 63) / 64;  // store instructions
   static_assert(!(CONTIG && (MODE == kTileDesc || SEG)), "descriptor tiles are strided");
-  static_assert(!SEG || (L == 1024 && (SPAN == 256 || (SPAN == 128 && !DO_POLY))),
-                "segments are 1 KiB, 256 B per lane (128 B: the XOR pass, which needs no r powers)");
+  static_assert(!SEG || (L == 1024 && (SPAN == 256 || SPAN == 128)),
+                "segments are 1 KiB, 256 or 128 B per lane");
   static_assert(NBUF == 1 || NBUF == 2, "one or two tile buffers");
   __shared__ uint4 lds[NBUF * C::NSLOT];
   const uint32_t lane = threadIdx.x;
@@ -370,7 +375,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
   if (SEG) {
     const uint64_t g = (uint64_t)blockIdx.x * 64 + lane;
     if (g < nrec) nxt_e = a.segs[dbase + g];
-    seg_meta_load<MODE>(nxt, a.rt, nxt_e, g < nrec, in, out);
+    seg_meta_load<MODE, SPAN>(nxt, a.rt, nxt_e, g < nrec, in, out);
   }
 
 #pragma unroll 1
@@ -394,7 +399,16 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) { kr[i] = nxt.r[i]; kss[i] = 0u; }
 #pragma unroll
-    for (int i = 0; i < 5; ++i) { pw[0].a[i] = nxt.pw16[i]; pw[C::LOG2G > 1 ? 1 : 0].a[i] = nxt.pw32[i]; }
+    for (int i = 0; i < 5; ++i) {  // r^BPL, r^(2 BPL), ...: 16, 32 (256-B spans) or 8, 16, 32 (128)
+      if (SPAN == 128) {
+        pw[0].a[i] = nxt.pw8[i];
+        pw[C::LOG2G > 1 ? 1 : 0].a[i] = nxt.pw16[i];
+        pw[C::LOG2G > 2 ? 2 : 0].a[i] = nxt.pw32[i];
+      } else {
+        pw[0].a[i] = nxt.pw16[i];
+        pw[C::LOG2G > 1 ? 1 : 0].a[i] = nxt.pw32[i];
+      }
+    }
     own_nlo = nxt.nlo;
     own_nhi = nxt.nhi;
     own_in_lo = nxt.in_lo; own_in_hi = nxt.in_hi;
@@ -491,7 +505,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     if (NBUF == 2 && prev_all) wait_vmcnt<NOUT>();
     else wait_vmem();
     wave_lds_fence();
-    if (SEG && t == 0) seg_meta_load<MODE>(nxt, a.rt, nxt_e, next0 + lane < nrec, in, out);
+    if (SEG && t == 0) seg_meta_load<MODE, SPAN>(nxt, a.rt, nxt_e, next0 + lane < nrec, in, out);
     if (NBUF == 2 && t + 1 < C::G) {  // the next tile's DMA now, into the other buffer
       const uint64_t nrec0 = rec0 + C::RPT;
       if (nrec0 < nrec) {

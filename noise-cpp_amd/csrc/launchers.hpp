@@ -16,11 +16,14 @@ hipError_t launch_aead_uniform(bool decrypt, const uint32_t key[8],
                                uint32_t ad_len, uint8_t *status, uint64_t nrec,
                                hipStream_t stream);
 
+// len_sum: the records' plaintext bytes (0 = unknown): a batch below the
+// classifier's record count whose records average >= 2 KiB is classified
+// anyway (one lane walking a 16 KiB record costs more than the classifier)
 hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
                                uint32_t nkeys, const noise_gpu_record *recs,
                                uint64_t nrec, const uint8_t *in, uint8_t *out,
                                const uint8_t *ad, uint8_t *status,
-                               hipStream_t stream);
+                               hipStream_t stream, uint64_t len_sum = 0);
 
 // zero the records-path scratch of (current device, stream)
 hipError_t records_scratch_wipe(hipStream_t stream);

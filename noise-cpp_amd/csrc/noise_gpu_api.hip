@@ -642,21 +642,28 @@ int noise_gpu_decrypt_uniform(const uint8_t h_key[32], uint64_t nonce0,
   return NOISE_GPU_OK;
 }
 
-int noise_gpu_encrypt_records(const uint8_t *d_keys, uint32_t nkeys,
-                              const noise_gpu_record *d_recs, uint64_t nrec,
-                              const uint8_t *d_in, uint8_t *d_out,
-                              const uint8_t *d_ad, void *stream) {
+static int records_dev(bool decrypt, const uint8_t *d_keys, uint32_t nkeys,
+                       const noise_gpu_record *d_recs, uint64_t nrec, const uint8_t *d_in,
+                       uint8_t *d_out, const uint8_t *d_ad, uint8_t *d_status, uint64_t len_sum,
+                       void *stream) {
   if (nrec == 0) return NOISE_GPU_OK;
-  if (!d_keys || !nkeys || !d_recs || !d_in || !d_out)
-    return arg_fail("null key table / descriptors / buffers");
+  if (!d_keys || !nkeys || !d_recs || !d_in || !d_out || (decrypt && !d_status))
+    return arg_fail(decrypt ? "null key table / descriptors / buffers / status"
+                            : "null key table / descriptors / buffers");
   if (reinterpret_cast<uintptr_t>(d_keys) & 15u)
     return arg_fail("key table must be 16-byte aligned");
   int rc = check_device();
   if (rc) return rc;
-  HIP_TRY(noise_amd::launch_aead_records(false, d_keys, nkeys, d_recs, nrec,
-                                         d_in, d_out, d_ad, nullptr,
-                                         (hipStream_t)stream));
+  HIP_TRY(noise_amd::launch_aead_records(decrypt, d_keys, nkeys, d_recs, nrec, d_in, d_out, d_ad,
+                                         decrypt ? d_status : nullptr, (hipStream_t)stream, len_sum));
   return NOISE_GPU_OK;
+}
+
+int noise_gpu_encrypt_records(const uint8_t *d_keys, uint32_t nkeys,
+                              const noise_gpu_record *d_recs, uint64_t nrec,
+                              const uint8_t *d_in, uint8_t *d_out,
+                              const uint8_t *d_ad, void *stream) {
+  return records_dev(false, d_keys, nkeys, d_recs, nrec, d_in, d_out, d_ad, nullptr, 0, stream);
 }
 
 int noise_gpu_decrypt_records(const uint8_t *d_keys, uint32_t nkeys,
@@ -664,17 +671,21 @@ int noise_gpu_decrypt_records(const uint8_t *d_keys, uint32_t nkeys,
                               const uint8_t *d_in, uint8_t *d_out,
                               const uint8_t *d_ad, uint8_t *d_status,
                               void *stream) {
-  if (nrec == 0) return NOISE_GPU_OK;
-  if (!d_keys || !nkeys || !d_recs || !d_in || !d_out || !d_status)
-    return arg_fail("null key table / descriptors / buffers / status");
-  if (reinterpret_cast<uintptr_t>(d_keys) & 15u)
-    return arg_fail("key table must be 16-byte aligned");
-  int rc = check_device();
-  if (rc) return rc;
-  HIP_TRY(noise_amd::launch_aead_records(true, d_keys, nkeys, d_recs, nrec,
-                                         d_in, d_out, d_ad, d_status,
-                                         (hipStream_t)stream));
-  return NOISE_GPU_OK;
+  return records_dev(true, d_keys, nkeys, d_recs, nrec, d_in, d_out, d_ad, d_status, 0, stream);
+}
+
+int noise_gpu_encrypt_records_sized(const uint8_t *d_keys, uint32_t nkeys,
+                                    const noise_gpu_record *d_recs, uint64_t nrec,
+                                    const uint8_t *d_in, uint8_t *d_out, const uint8_t *d_ad,
+                                    uint64_t len_sum, void *stream) {
+  return records_dev(false, d_keys, nkeys, d_recs, nrec, d_in, d_out, d_ad, nullptr, len_sum, stream);
+}
+
+int noise_gpu_decrypt_records_sized(const uint8_t *d_keys, uint32_t nkeys,
+                                    const noise_gpu_record *d_recs, uint64_t nrec,
+                                    const uint8_t *d_in, uint8_t *d_out, const uint8_t *d_ad,
+                                    uint8_t *d_status, uint64_t len_sum, void *stream) {
+  return records_dev(true, d_keys, nkeys, d_recs, nrec, d_in, d_out, d_ad, d_status, len_sum, stream);
 }
 
 static int sessions(bool decrypt, const uint8_t *d_keys, uint32_t nkeys,
@@ -905,11 +916,13 @@ static int records_host(bool decrypt, const uint8_t *h_keys, uint32_t nkeys,
   hipError_t e = hipMemcpyAsync(s.d, s.h, o_out, hipMemcpyHostToDevice, s.stream);
   if (e == hipSuccess && ad_bytes)
     e = hipMemcpyAsync(s.d + o_ad, s.h + o_ad, ad_bytes, hipMemcpyHostToDevice, s.stream);
+  uint64_t len_sum = 0;  // the descriptors are on the host here: the batch's size
+  for (uint64_t i = 0; i < nrec; ++i) len_sum += h_recs[i].len;
   if (e == hipSuccess)
     e = noise_amd::launch_aead_records(
         decrypt, s.d + o_keys, nkeys,
         reinterpret_cast<const noise_gpu_record *>(s.d + o_recs), nrec, s.d + o_in,
-        s.d + o_out, s.d + o_ad, decrypt ? s.d + o_st : nullptr, s.stream);
+        s.d + o_out, s.d + o_ad, decrypt ? s.d + o_st : nullptr, s.stream, len_sum);
   if (e == hipSuccess)
     e = hipMemcpyAsync(s.h + o_out, s.d + o_out, o_st + nrec - o_out, hipMemcpyDeviceToHost,
                        s.stream);

@@ -57,6 +57,10 @@ constexpr int kCols = kNumCls + 2 + kFinBuckets;
 #define NOISE_SEG_CHUNKS 4
 #endif
 constexpr int kSegChunks = NOISE_SEG_CHUNKS;
+#ifndef NOISE_CHUNK_MIN  // overridable for the CPU emulation build
+#define NOISE_CHUNK_MIN 65536
+#endif
+constexpr uint64_t kChunkMinRecords = NOISE_CHUNK_MIN;  // smaller batches: one chunk
 // finalize lanes per long record
 #ifndef NOISE_FIN_W
 #define NOISE_FIN_W 4
@@ -76,6 +80,7 @@ constexpr int kSegChunks = NOISE_SEG_CHUNKS;
 #define NOISE_CLASSIFY_MIN 2048
 #endif
 constexpr uint64_t kClassifyMin = NOISE_CLASSIFY_MIN;
+constexpr uint64_t kClassifyAvgLen = 2048;  // below kClassifyMin: classify when records average this
 constexpr uint32_t kLongMax = 65535;      // the Noise message bound
 #ifndef NOISE_SEG_CAP  // overridable for the CPU emulation build (overflow path)
 #define NOISE_SEG_CAP (1ull << 24)
@@ -930,7 +935,7 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
                                  const uint32_t *tails, const uint32_t *fin, uint64_t segbound,
                                  const uint8_t *in,
                                  uint8_t *out, const uint8_t *ad, uint8_t *status,
-                                 hipStream_t stream) {
+                                 hipStream_t stream, int chunks) {
   AuxStream ax;
   hipError_t e = aux_get(&ax, stream);
   if (e != hipSuccess) return e;
@@ -989,26 +994,30 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   // also waits for the tails' P_tail).  The checks sit here, not in front of
   // the keystream passes, so chunk c + 1's is done while chunk c's plaintext
   // is being written and the keystream passes follow each other without gaps
+  // (one chunk: the whole range, c = -1: no split table, the finalize in the
+  // classifier's bucket order)
   TileArgs ac = a;
-  ac.seg_split = hdr->ssplit;
-  for (int c = 0; c < kSegChunks; ++c) {
-    ac.chunk = c;
+  ac.seg_split = chunks > 1 ? hdr->ssplit : nullptr;
+  auto cidx = [chunks](int c) { return chunks > 1 ? c : -1; };
+  for (int c = 0; c < chunks; ++c) {
+    ac.chunk = cidx(c);
     hipLaunchKernelGGL((k_aead_tile<true, 1024, false, kTileSegPoly, 0, 1, NOISE_POLY_SPAN>), gseg, bt, 0,
                        stream, ac);
     if (c == 0 && (e = hipStreamWaitEvent(stream, ax.join, 0)) != hipSuccess) return e;
     hipLaunchKernelGGL((k_seg_finalize_w<true, NOISE_FIN_W>), gfin, bt, 0, stream, fin, rt, ta.partial,
-                       ta.partial_hi, hdr_w, in, out, status, c);
+                       ta.partial_hi, hdr_w, in, out, status, cidx(c));
     if ((e = hipEventRecord(ax.fin[c], stream)) != hipSuccess) return e;
   }
   // companion 2: the segments' plaintext, chunk by chunk; the companion
   // writes each chunk's tails' plaintext beside it
-  for (int c = 0; c < kSegChunks; ++c) {
-    ac.chunk = c;
+  for (int c = 0; c < chunks; ++c) {
+    ac.chunk = cidx(c);
     if ((e = hipStreamWaitEvent(ax.aux2, ax.fin[c], 0)) != hipSuccess) return e;
     hipLaunchKernelGGL((k_aead_tile<true, 1024, false, kTileSegXor, 0, 1, NOISE_XOR_SPAN>), gseg, bt, 0,
                        ax.aux2, ac);
     if ((e = hipStreamWaitEvent(ax.aux, ax.fin[c], 0)) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_seg_tail<true, kTailXor>), grid, bt, 0, ax.aux, tails, rt, hdr, in, out, c);
+    hipLaunchKernelGGL((k_seg_tail<true, kTailXor>), grid, bt, 0, ax.aux, tails, rt, hdr, in, out,
+                       cidx(c));
   }
 #undef NOISE_DESC_TILE
 #undef NOISE_DESC_TILES
@@ -1023,11 +1032,17 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
                                uint32_t nkeys, const noise_gpu_record *recs,
                                uint64_t nrec, const uint8_t *in, uint8_t *out,
                                const uint8_t *ad, uint8_t *status,
-                               hipStream_t stream) {
+                               hipStream_t stream, uint64_t len_sum) {
   if (nrec == 0) return hipSuccess;
   const dim3 bg(kGenBlock);
   const uint64_t gblocks = (nrec + kGenBlock - 1) / kGenBlock;
-  if (nrec < kClassifyMin) {
+  // Few records: the generic kernel alone (the classifier and the class
+  // kernels cost ~0.13 ms per call in launches and stream joins), unless they
+  // are long: one lane walks a record, ~19 us per KiB.  Same box (round 4,
+  // tools/bench_small_records.py, enc + dec): 300 x 64 B 17 us generic / 262
+  // classified; 300 x 1 KiB 97 / 282; 100 x 16 KiB 1909 / 353.
+  const bool few = nrec < kClassifyMin && !(len_sum && len_sum / nrec >= kClassifyAvgLen);
+  if (few) {
     if (decrypt)
       hipLaunchKernelGGL((k_aead_records<true>), dim3((unsigned)gblocks), bg, 0, stream, keys, nkeys, recs, nrec, nullptr, nullptr, in, out, ad, status);
     else
@@ -1090,10 +1105,13 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   ta.partial = partial;
   ta.partial_hi = partial_hi;
   ta.nseg = &hdr->nseg;
+  // the decrypt pipeline's chunks pay off on large batches only (each chunk
+  // adds four launches and a stream hand-off)
+  const int chunks = nrec >= kChunkMinRecords ? kSegChunks : 1;
   return decrypt ? launch_classes<true>(ta, nrec, hdr, keys, nkeys, recs, idx, tails, fin, segcap,
-                                       in, out, ad, status, stream)
+                                       in, out, ad, status, stream, chunks)
                  : launch_classes<false>(ta, nrec, hdr, keys, nkeys, recs, idx, tails, fin, segcap,
-                                         in, out, ad, status, stream);
+                                         in, out, ad, status, stream, 1);
 }
 
 }  // namespace noise_amd

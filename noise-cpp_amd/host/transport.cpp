@@ -695,10 +695,14 @@ void Pipeline::enqueue(const LaunchJob &j) {
     hip_check(hipMemcpyAsync(sl.d + o_in_, sl.h + o_in_, sl.in_used, hipMemcpyHostToDevice, sl.st),
               "messages H2D");
   const auto *d_recs = reinterpret_cast<const noise_gpu_record *>(sl.d);
-  const int rc = dec ? noise_gpu_decrypt_records(d_keys_, (std::uint32_t)j.nkeys, d_recs, sl.nrec, sl.d + o_in_,
-                                                 sl.d + o_out_, nullptr, sl.d + o_st_, sl.st)
-                     : noise_gpu_encrypt_records(d_keys_, (std::uint32_t)j.nkeys, d_recs, sl.nrec, sl.d + o_in_,
-                                                 sl.d + o_out_, nullptr, sl.st);
+  // the slot's plaintext bytes (the padded out / in images bound them):
+  // lets a slot of few long messages take the load-balanced path
+  const std::uint64_t len_sum = dec ? sl.out_used : sl.in_used;
+  const int rc = dec ? noise_gpu_decrypt_records_sized(d_keys_, (std::uint32_t)j.nkeys, d_recs, sl.nrec,
+                                                       sl.d + o_in_, sl.d + o_out_, nullptr, sl.d + o_st_,
+                                                       len_sum, sl.st)
+                     : noise_gpu_encrypt_records_sized(d_keys_, (std::uint32_t)j.nkeys, d_recs, sl.nrec,
+                                                       sl.d + o_in_, sl.d + o_out_, nullptr, len_sum, sl.st);
   if (rc != NOISE_GPU_OK)
     throw std::runtime_error(std::string("noise-mi355x: ") + noise_gpu_strerror(rc) + ": " +
                              noise_gpu_last_error());

@@ -48,6 +48,7 @@ def _run(binary, mode, nrec, seed, gap):
 
 @pytest.mark.parametrize("mode,nrec,seed,gap", [
     ("cfg4", 700, 4, 0),
+    ("cfg4", 2500, 8, 0),   # >= 1000 records (emulation build): the chunked decrypt pipeline
     ("inplace", 500, 5, (2 << 30) + 4096),
     ("ragged", 300, 6, 0),
 ])

@@ -159,19 +159,34 @@ def latest_profile(cfg):
     return best
 
 
-def pmc_kernels(prof, names):
+def pmc_kernels(prof, names, anchor=None):
     """Sum the per-dispatch PMC means of the kernels whose symbol starts with
-    one of `names` (one launch each per call)."""
+    one of `names`, per call: a kernel launched k times per call (the
+    decrypt pipeline's chunks) counts k times -- its dispatches in the
+    profiled run over those of `anchor`, a kernel launched once per call of
+    this direction (kernels both directions launch, over both anchors)."""
     if not prof:
         return None
     ks = prof[1]["kernels"]
-    rows = [v for k, v in ks.items() if any(k.startswith(n) for n in names)]
+    rows = [(k, v) for k, v in ks.items() if any(k.startswith(n) for n in names)]
     if not rows:
         return None
+
+    def calls(k):
+        if not anchor or "_dispatches" not in ks.get(anchor, {}):
+            return None
+        if "<true" in k or "<false" in k:
+            return ks[anchor]["_dispatches"]
+        other = anchor.replace("<true", "<false") if "<true" in anchor else anchor.replace("<false", "<true")
+        return ks[anchor]["_dispatches"] + ks.get(other, {}).get("_dispatches", 0)
+
     out = {}
-    for r in rows:
+    for k, r in rows:
+        n = calls(k)
+        f = r["_dispatches"] / n if n and r.get("_dispatches") else 1.0
         for c, v in r.items():
-            out[c] = out.get(c, 0.0) + v
+            if c != "_dispatches":
+                out[c] = out.get(c, 0.0) + v * f
     return out
 
 
@@ -553,7 +568,8 @@ def make_workload(cfg, args, rank, world, stream):
                            ("noise_amd::k_cls_", "noise_amd::k_seg_prep", "noise_amd::k_seg_tail<true",
                             "noise_amd::k_seg_finalize_w<true", "noise_amd::k_aead_tile<true",
                             "noise_amd::k_aead_records<true")),
-                "call_level": True, "oracle": oracle}
+                "call_level": True, "oracle": oracle,
+                "pmc_anchor": ("noise_amd::k_aead_records<false>", "noise_amd::k_aead_records<true>")}
     else:
         raise SystemExit("unknown config %d" % cfg)
 
@@ -793,7 +809,7 @@ def roofline(cfg, wl, enc_ms, dec_ms):
     names = wl["knames"][d]
     achieved = kbytes / (kms * 1e-3)
     prof = latest_profile(cfg)
-    pmc = pmc_kernels(prof, names)
+    pmc = pmc_kernels(prof, names, wl.get("pmc_anchor", (None, None))[d])
     # the profile's per-launch counts, scaled to this launch's records (a
     # strong-scaling shard, or --records, launches fewer than were profiled)
     scale = 1.0

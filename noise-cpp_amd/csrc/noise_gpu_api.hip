@@ -370,6 +370,9 @@ struct OneCtx {
     if (rstream) return NOISE_GPU_OK;
     int least = 0, greatest = 0;
     HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+#ifdef NOISE_RES_NORMAL_PRIO  // A/B only: a normal-priority stream (shares a queue with the others)
+    greatest = least;
+#endif
     HIP_TRY(hipStreamCreateWithPriority(&rstream, hipStreamNonBlocking, greatest));
     return NOISE_GPU_OK;
   }

@@ -853,12 +853,13 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_resident(uint8_t *req, uint8
           if (__ballot((need0 && c.x != seq) || (need1 && c1.x != seq)) == 0ull) {
             // every chunk carries seq; the words must also sum to the check
             // word (launchers.hpp req_check_mix), else a chunk landed in part
+            // (DPP row sums + 4 readlanes: a chain of LDS-crossbar shuffles
+            // here cost ~0.5 us per request)
             uint32_t v = 0u;
             if (lane < 4u || need0) v = req_check_mix(lane, c.y, c.z, lane == 3u ? 0u : c.w);
             if (need1) v += req_check_mix(64u + lane, c1.y, c1.z, c1.w);
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) v += (uint32_t)__shfl_xor((int)v, d);
-            if (v + kReqCheckSalt == (uint32_t)__shfl((int)c.w, 3)) {
+            v = rows_total(row_sum_dpp(v));
+            if (v + kReqCheckSalt == (uint32_t)__builtin_amdgcn_readlane((int)c.w, 3)) {
               NOISE_ONE_STAMP(0);
               break;
             }

@@ -48,6 +48,12 @@ for i in range(1, 10):
     for r in csv.DictReader(open(f)):
         agg[symbol(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
 summary = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in agg.items()}
+# dispatches of each kernel in one PMC pass (a kernel launched more than once
+# per call -- the decrypt pipeline's chunks -- counts that many times per
+# call: bench.py scales its per-dispatch means by the ratio to a
+# once-per-call kernel)
+for k, d in agg.items():
+    summary[k]["_dispatches"] = max(len(v) for v in d.values()) if d else 0
 bench_line = None
 for f in ("bench_trace.json", "bench_pmc1.json"):
     p = os.path.join(src, f)

@@ -61,6 +61,7 @@ constexpr int kSegChunks = NOISE_SEG_CHUNKS;
 #define NOISE_CHUNK_MIN 65536
 #endif
 constexpr uint64_t kChunkMinRecords = NOISE_CHUNK_MIN;  // smaller batches: one chunk
+constexpr int kHdrWords = kSegChunks <= 4 ? 64 : 256;    // scratch header: 512 B (2 KiB)
 // finalize lanes per long record
 #ifndef NOISE_FIN_W
 #define NOISE_FIN_W 4
@@ -137,9 +138,9 @@ struct RecHdr {
   // ssplit[c + 1]) (k_cls_scatter; clamped to nlong / nseg where used)
   // and tails [tsplit[c], tsplit[c + 1]) (clamped to the tail count)
   unsigned long long qsplit[kSegChunks + 1], ssplit[kSegChunks + 1], tsplit[kSegChunks + 1];
-  unsigned long long pad[61 - 2 * kCols - 3 * (kSegChunks + 1)];
+  unsigned long long pad[kHdrWords - 3 - 2 * kCols - 3 * (kSegChunks + 1)];
 };
-static_assert(sizeof(RecHdr) == 512, "scratch header layout");
+static_assert(sizeof(RecHdr) == 8 * kHdrWords, "scratch header layout");
 
 // finalize-order bucket of a long record with nf >= 1 full segments
 __device__ __forceinline__ int fin_bucket(uint32_t nf) {

@@ -26,8 +26,8 @@
 // wave, so no s_barrier is needed: LDS ordering is program order within the
 // wave (the fences below only stop the compiler from moving LDS accesses).
 // LDS image per tile: RPT*L/16 16-byte slots (plaintext/ciphertext, XOR-
-// swizzled within 16-slot groups so the per-lane ds_read/ds_write_b128 are
-// bank-conflict free) + RPT tag slots.  The swizzle is applied on the
+// swizzled (swz) so the per-lane ds_read/ds_write_b128 are bank-conflict
+// free) + RPT tag slots.  The swizzle is applied on the
 // global SOURCE address of the LDS-DMA (its LDS destination is lane-linear).
 #pragma once
 #include "chachapoly_device.hpp"
@@ -52,8 +52,26 @@ struct TileCfg {
   static_assert(G == 1 || BPL == 8 || BPL == 16, "span of 128 or 256 bytes");
 };
 
-// slot <-> piece involution inside each aligned 16-slot group
-__device__ __forceinline__ uint32_t swz(uint32_t s) { return s ^ ((s >> 4) & 15u); }
+// slot <-> piece involution (gfx950 banking: ds_read_b128 in four 16-lane
+// groups over 16 slots of 16 B, ds_write_b128 in eight 8-lane groups over 8).
+// SPAN 256 (lanes 4 apart share a record): XOR within each aligned 16-slot
+// group by slot bits 4..7 -- lane l's span starts at slot 16l.  SPAN 128
+// (lane l's span at slot 8l): XOR of bits 0..2 by bits 3..5 ^ 6..8, which
+// keeps the 8-lane write groups conflict free as well (the 256-B form leaves
+// lanes 2k, 2k+1 on one bank of a ds_write_b128: 2-way, 8.7 M extra LDS
+// cycles per keystream-pass launch in config 4).
+template <int SPAN>
+__device__ __forceinline__ uint32_t swz(uint32_t s) {
+  if constexpr (SPAN == 128) return s ^ (((s >> 3) ^ (s >> 6)) & 7u);
+  else return s ^ ((s >> 4) & 15u);
+}
+// swz(64q + lane) - 64q from gl[i] = swz(64i + lane) - 64i: it depends on q
+// only through q & 3 (SPAN 256), or is gl[0] ^ (q & 7) (SPAN 128)
+template <int SPAN>
+__device__ __forceinline__ uint32_t glq(const uint32_t gl[4], int q) {
+  if constexpr (SPAN == 128) return gl[0] ^ ((uint32_t)q & 7u);
+  else return gl[q & 3];
+}
 
 // LDS-typed pointer for the LDS-DMA destinations.  Taking it straight from
 // the __shared__ array (instead of casting a generic pointer inside a
@@ -175,7 +193,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
   constexpr bool TAGGED_IN = DECRYPT && MODE < kTileSeg;  // ct || tag pieces
   constexpr int IN_SLOTS = TAGGED_IN ? C::NSLOT : C::REC_SLOTS;
   if (CONTIG) {
-    // slot s = 64q + lane holds piece swz(s) = 64q + gl[q & 3]; packed
+    // slot s = 64q + lane holds piece swz(s) = 64q + glq(gl, q); packed
     // records put piece g of an encrypt tile at byte 16g and of a decrypt
     // tile (SPR+1 pieces per record) at 16(g + g/SPR).
     const uint8_t *base = in + rec0 * in_stride;  // wave-uniform
@@ -185,14 +203,14 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
       // two taken branches around each of the REC_SLOTS / 64 DMAs
 #pragma unroll
       for (int q = 0; q < C::REC_SLOTS / 64; ++q) {
-        const uint32_t g = 64u * q + gl[q & 3];
+        const uint32_t g = 64u * q + glq<SPAN>(gl, q);
         const uint32_t rr = g / C::SPR;
         lds_dma16_s(base, DECRYPT ? 16u * (g + rr) : 16u * g, (lds_void *)(lds3 + 64 * q));
       }
     } else {
 #pragma unroll
       for (int q = 0; q < C::REC_SLOTS / 64; ++q) {
-        const uint32_t g = 64u * q + gl[q & 3];
+        const uint32_t g = 64u * q + glq<SPAN>(gl, q);
         const uint32_t rr = g / C::SPR;
         const uint32_t off = DECRYPT ? 16u * (g + rr) : 16u * g;
         if (rr < nv) lds_dma16_s(base, off, (lds_void *)(lds3 + 64 * q));
@@ -217,7 +235,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
         const uint32_t kl = t_rpt + q;
         const uint64_t off = join64((uint32_t)__builtin_amdgcn_readlane((int)own_in_hi, (int)kl),
                                     (uint32_t)__builtin_amdgcn_readlane((int)own_in_lo, (int)kl));
-        lds_dma16_s(in + off, 16u * gl[q & 3], (lds_void *)(lds3 + 64 * q));
+        lds_dma16_s(in + off, 16u * glq<SPAN>(gl, q), (lds_void *)(lds3 + 64 * q));
       }
     }
     if (TAGGED_IN) {  // decrypt: the RPT tags, lane r -> slot REC_SLOTS + r
@@ -233,7 +251,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
       const uint32_t s = 64u * q + lane;
       uint32_t r, p;
       if (s < (uint32_t)C::REC_SLOTS) {
-        const uint32_t g = swz(s);
+        const uint32_t g = swz<SPAN>(s);
         r = g / C::SPR;
         p = g % C::SPR;
       } else {  // decrypt: tag slots
@@ -360,10 +378,10 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
   for (int i = 0; i < 8; ++i) k[i] = a.key.w[i];
 
   const uint32_t rho = lane / C::G, j = lane % C::G;
-  // swz(64q + lane) - 64q depends on q only through q & 3
+  // swz(64q + lane) - 64q (glq)
   uint32_t gl[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) gl[i] = swz(64u * i + lane) - 64u * i;
+  for (int i = 0; i < 4; ++i) gl[i] = swz<SPAN>(64u * i + lane) - 64u * i;
 
   // kTileSeg: each super-tile's per-segment metadata (SegEntry -> SegRec,
   // two dependent loads) is fetched one super-tile ahead -- the SegEntry with
@@ -567,7 +585,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
       if (DO_XOR && kk + 1 < C::CPL) chacha20_block_pre(kt, cb + 1u + kk, pre, n_lo, n_hi, ksn);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const uint32_t slot = swz(rho * C::SPR + 4u * c + q);
+        const uint32_t slot = swz<SPAN>(rho * C::SPR + 4u * c + q);
         const uint4 v = lb[slot];
         uint4 o = v;
         if (DO_XOR) {
@@ -699,7 +717,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
         if (q < NDATA) {
           r = (uint32_t)q / (C::SPR / 64);
           pc = 64u * ((uint32_t)q % (C::SPR / 64)) + lane;
-          slot = swz(64u * q + lane);  // == swz(r * SPR + pc)
+          slot = swz<SPAN>(64u * q + lane);  // == swz(r * SPR + pc)
           ok = true;
         } else {
           r = lane < (uint32_t)C::RPT ? lane : 0u;
@@ -711,7 +729,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
       }
       if (RECQ) {
         if (q < C::RPT) {
-          r = (uint32_t)q; pc = lane; slot = swz(64u * q + lane); ok = true;
+          r = (uint32_t)q; pc = lane; slot = swz<SPAN>(64u * q + lane); ok = true;
         } else {
           r = lane < (uint32_t)C::RPT ? lane : 0u; pc = C::SPR; slot = C::REC_SLOTS + r;
           ok = lane < (uint32_t)C::RPT;
@@ -721,8 +739,8 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
       const uint32_t g = 64u * q + lane;  // output piece (record r, piece pc)
       r = g / OPR;
       pc = g % OPR;
-      if (CONTIG && DECRYPT) slot = 64u * q + gl[q & 3];  // == swz(g)
-      else slot = pc < (uint32_t)C::SPR ? swz(r * C::SPR + pc) : C::REC_SLOTS + r;
+      if (CONTIG && DECRYPT) slot = 64u * q + glq<SPAN>(gl, q);  // == swz(g)
+      else slot = pc < (uint32_t)C::SPR ? swz<SPAN>(r * C::SPR + pc) : C::REC_SLOTS + r;
       ok = OUT_SLOTS % 64 == 0 || g < (uint32_t)OUT_SLOTS;
     };
 #pragma unroll

@@ -173,7 +173,7 @@ static int run_pipeline(int S, int M, std::uint64_t seed) {
 // tiny slots its serial walk
 static int run_pipeline_batch(int S, int M, std::uint64_t seed, std::size_t slot_records = 97,
                               std::size_t slot_bytes = 256 << 10, std::size_t maxlen = 3000,
-                              int maxbatch = 300, int threads = 4) {
+                              int maxbatch = 300, int threads = 4, int big_every = 29) {
   std::mt19937_64 rng(seed);
   int fails = 0;
   auto check = [&](bool c, const char *what, long i) {
@@ -200,7 +200,8 @@ static int run_pipeline_batch(int S, int M, std::uint64_t seed, std::size_t slot
   std::vector<bytes> pt(M), ct(M), back(M);
   std::vector<nt::Pipeline::Message> msgs(M);
   for (int i = 0; i < M; ++i) {
-    pt[i].resize(rng() % 29 == 0 ? 65519 : rng() % maxlen);
+    // every ~big_every-th message is a maximum-size one (0: none)
+    pt[i].resize(big_every > 0 && rng() % (unsigned)big_every == 0 ? 65519 : rng() % maxlen);
     for (auto &b : pt[i]) b = (std::uint8_t)rng();
     msgs[i] = {(std::size_t)(rng() % S), pt[i].data(), pt[i].size()};
   }
@@ -689,7 +690,7 @@ int main(int argc, char **argv) {
       return run_pipeline_batch(std::atoi(argv[2]), std::atoi(argv[3]), std::strtoull(argv[4], nullptr, 0),
                                 std::strtoull(argv[5], nullptr, 0), std::strtoull(argv[6], nullptr, 0),
                                 std::strtoull(argv[7], nullptr, 0), std::atoi(argv[8]),
-                                argc > 9 ? std::atoi(argv[9]) : 4);
+                                argc > 9 ? std::atoi(argv[9]) : 4, argc > 10 ? std::atoi(argv[10]) : 29);
     return run_pipeline_batch(std::atoi(argv[2]), std::atoi(argv[3]), std::strtoull(argv[4], nullptr, 0));
   }
   if (argc > 1 && std::string(argv[1]) == "bench")

@@ -81,7 +81,7 @@ constexpr int kHdrWords = kSegChunks <= 4 ? 64 : 256;    // scratch header: 512 
 // 4), or 0 = the three-pass segment pipeline (kTileSegPoly, finalize,
 // kTileSegXor in kSegChunks chunks)
 #ifndef NOISE_REC_DEC_W
-#define NOISE_REC_DEC_W 4
+#define NOISE_REC_DEC_W 1
 #endif
 #ifndef NOISE_CLASSIFY_MIN  // overridable for the CPU emulation build
 #define NOISE_CLASSIFY_MIN 2048
@@ -722,15 +722,15 @@ __global__ __launch_bounds__(64 * W) void k_rec_dec(const uint32_t *__restrict__
                                                      uint8_t *status) {
   static_assert(W == 1 || W == 2 || W == 4, "1, 2 or 4 waves per record");
   constexpr uint32_t T = 64u * W;
-  __shared__ uint4 tile[W * 256];
+  __shared__ uint4 tile[W * 512];  // per wave: two 4 KiB keystream tiles
   __shared__ uint32_t red[W * 5];
   __shared__ unsigned long long item;
   // wv through readfirstlane: the wave's LDS tile address is then an SGPR
   // value (the LDS-DMA takes it in M0)
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = uniform32(tid >> 6);
   const uint64_t nfin = hdr->counts[kClsLong], nlong = hdr->nlong;
-  uint4 *lt = tile + 256u * wv;
-  lds_u4 *lt3 = NOISE_LDS3(tile) + 256u * wv;
+  uint4 *lt = tile + 512u * wv;
+  lds_u4 *lt3 = NOISE_LDS3(tile) + 512u * wv;
 #pragma unroll 1
   for (;;) {
     if (tid == 0) item = atomicAdd(&hdr->spare0, 1ull);
@@ -767,37 +767,70 @@ __global__ __launch_bounds__(64 * W) void k_rec_dec(const uint32_t *__restrict__
 #pragma unroll
     for (int i = 0; i < 5; ++i) acc.a[i] = 0u;
     const int64_t i0 = (int64_t)tid - (int64_t)pad;
-#pragma unroll 1
-    for (uint32_t c0 = 0; c0 < C; c0 += 4) {
-      uint4 m[4];
-      uint32_t hib[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {  // the four steps' loads first
-        const int64_t i = i0 + (int64_t)(c0 + u) * T;
-        m[u] = make_uint4(0u, 0u, 0u, 0u);
-        hib[u] = 0u;
-        if (c0 + u < C) {
-          if (i >= 0 && i < (int64_t)nb) {
-            const u32x4 v = *(const g_u32x4 *)(src + 16 * i);
-            m[u] = make_uint4(v.x, v.y, v.z, v.w);
-            hib[u] = 1u;
-          } else if (i == (int64_t)nb) {  // LE64(ad_len = 0) || LE64(len)
-            m[u] = make_uint4(0u, 0u, len, 0u);
-            hib[u] = 1u;
-          }
+    // lane's block of step c: a ciphertext block, the length block, or a
+    // front-pad zero (hib 0: no 2^128 bit)
+    auto blk = [&](uint32_t c, uint4 &m, uint32_t &hib) {
+      const int64_t i = i0 + (int64_t)c * T;
+      m = make_uint4(0u, 0u, 0u, 0u);
+      hib = 0u;
+      if (c < C) {
+        if (i >= 0 && i < (int64_t)nb) {
+          const u32x4 v = *(const g_u32x4 *)(src + 16 * i);
+          m = make_uint4(v.x, v.y, v.z, v.w);
+          hib = 1u;
+        } else if (i == (int64_t)nb) {  // LE64(ad_len = 0) || LE64(len)
+          m = make_uint4(0u, 0u, len, 0u);
+          hib = 1u;
         }
       }
+    };
+    // two batches of kB steps in flight: batch b + 1's loads go out before
+    // batch b's products
+    constexpr uint32_t kB = 4;
+    uint4 ma[kB], mb[kB];
+    uint32_t ha[kB], hb[kB];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+    for (uint32_t u = 0; u < kB; ++u) blk(u, ma[u], ha[u]);
+#pragma unroll 1
+    for (uint32_t c0 = 0; c0 < C; c0 += kB) {
+#pragma unroll
+      for (uint32_t u = 0; u < kB; ++u) blk(c0 + kB + u, mb[u], hb[u]);
+#pragma unroll
+      for (uint32_t u = 0; u < kB; ++u) {
         if (c0 + u >= C) break;
         const int64_t i = i0 + (int64_t)(c0 + u) * T;
-        if (i == (int64_t)nb - 1 && (len & 15u)) m[u] = mask_bytes(m[u], (int)(len & 15u));
+        uint4 m = ma[u];
+        if (i == (int64_t)nb - 1 && (len & 15u)) m = mask_bytes(m, (int)(len & 15u));
         acc = mul26(acc, Rs);
-        const F26 x = to26(m[u].x, m[u].y, m[u].z, m[u].w, hib[u]);
+        const F26 x = to26(m.x, m.y, m.z, m.w, ha[u]);
 #pragma unroll
         for (int k = 0; k < 5; ++k) acc.a[k] += x.a[k];
       }
+#pragma unroll
+      for (uint32_t u = 0; u < kB; ++u) {
+        ma[u] = mb[u];
+        ha[u] = hb[u];
+      }
     }
+    // The keystream pass's first tile now (a load: nothing of the record is
+    // stored before its tag is checked), so it lands during the sums below.
+    // Every tile DMA issues all 4 instructions (pieces past the record read
+    // its last one instead) so that the counted waits below stay exact.
+    const uint32_t ntile = (len + 4095u) >> 12, lastp = 16u * (nb - 1u);
+    const uint64_t ga = (uint64_t)(uintptr_t)src;
+    const uint8_t *gsrc = (const uint8_t *)(uintptr_t)join64(uniform32((uint32_t)(ga >> 32)),
+                                                             uniform32((uint32_t)ga));
+    auto dma = [&](uint32_t t, uint32_t buf) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t off = (t << 12) + 16u * rswz(64u * j + lane);
+        lds_dma16_s(gsrc, off < len ? off : lastp, (lds_void *)(lt3 + 256u * buf + 64u * j));
+      }
+    };
+    wait_lds();  // the previous record's last LDS reads are done
+    wave_lds_fence();
+    if (wv < ntile) dma(wv, 0u);
+
     // sum over the wave's lanes: S = sum_L acc_L r^(63 - L), then times r
     F26 S = acc;
 #pragma unroll
@@ -850,6 +883,7 @@ __global__ __launch_bounds__(64 * W) void k_rec_dec(const uint32_t *__restrict__
 
     // ---- 3. plaintext ---------------------------------------------------
     if (!ok) {  // no plaintext leaves: in place untouched, a copy zeroed
+      wait_vmem();  // the prefetched tile has landed before its buffer is reused
       if (src != dst)
 #pragma unroll 1
         for (uint32_t off = 16u * tid; off < len; off += 16u * T) {
@@ -864,35 +898,34 @@ __global__ __launch_bounds__(64 * W) void k_rec_dec(const uint32_t *__restrict__
     for (int i = 0; i < 8; ++i) k[i] = R.k[i];
     const uint32_t n_lo = (uint32_t)R.nonce, n_hi = (uint32_t)(R.nonce >> 32);
     const ChaPre pre = chacha_pre(k, n_lo, n_hi);
-    const uint32_t ntile = (len + 4095u) >> 12;
+    uint32_t buf = 0u;
 #pragma unroll 1
-    for (uint32_t t = wv; t < ntile; t += W) {
-      const uint32_t base = t << 12;
-      wait_lds();  // the previous tile's LDS reads are done before the DMA lands
+    for (uint32_t t = wv; t < ntile; t += W, buf ^= 1u) {
+      // the next tile's DMA into the other buffer (its last reader, tile
+      // t - W's store loop, is done: lgkmcnt), then wait for all but it
+      wait_lds();
       wave_lds_fence();
-      // the tile's global base as a wave-uniform (SGPR) operand of the DMA
-      const uint64_t ga = (uint64_t)(uintptr_t)(src + base);
-      const uint8_t *gbase = (const uint8_t *)(uintptr_t)join64(uniform32((uint32_t)(ga >> 32)),
-                                                                uniform32((uint32_t)ga));
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t pc = rswz(64u * j + lane);
-        if (base + 16u * pc < len) lds_dma16_s(gbase, 16u * pc, (lds_void *)(lt3 + 64 * j));
+      if (t + W < ntile) {
+        dma(t + W, buf ^ 1u);
+        wait_vmcnt<4>();
+      } else {
+        wait_vmem();
       }
-      wait_vmem();
       wave_lds_fence();
+      uint4 *lb = lt + 256u * buf;
+      const uint32_t base = t << 12;
       if (base + 64u * lane < len) {
         uint32_t ks[16];
         chacha20_block_pre(k, 1u + (base >> 6) + lane, pre, n_lo, n_hi, ks);
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
           const uint32_t slot = rswz(4u * lane + kk);
-          uint4 v = lt[slot];
+          uint4 v = lb[slot];
           v.x ^= ks[4 * kk + 0];
           v.y ^= ks[4 * kk + 1];
           v.z ^= ks[4 * kk + 2];
           v.w ^= ks[4 * kk + 3];
-          lt[slot] = v;
+          lb[slot] = v;
         }
       }
       wave_lds_fence();
@@ -900,7 +933,7 @@ __global__ __launch_bounds__(64 * W) void k_rec_dec(const uint32_t *__restrict__
       for (int j = 0; j < 4; ++j) {
         const uint32_t pc = 64u * j + lane, off = base + 16u * pc;
         if (off < len) {
-          const uint4 v = lt[rswz(pc)];
+          const uint4 v = lb[rswz(pc)];
           const uint32_t n = len - off;
           if (n >= 16u) store16<true>(dst + off, v, 16);
           else store16<false>(dst + off, v, (int)n);

@@ -715,8 +715,15 @@ __device__ __forceinline__ uint32_t rswz(uint32_t s) {
   return s ^ (((s >> 4) & 1u) | ((((s >> 3) ^ (s >> 5)) & 1u) << 1));
 }
 
+#if defined(NOISE_HIP_EMU)
+#define NOISE_WAVES_PER_EU(n)
+#else
+#define NOISE_WAVES_PER_EU(n) __attribute__((amdgpu_waves_per_eu(n)))
+#endif
+// 4 waves per SIMD (<= 128 VGPRs): the Poly1305 pass waits on its loads,
+// and other waves' keystream work fills those waits
 template <int W>
-__global__ __launch_bounds__(64 * W) void k_rec_dec(const uint32_t *__restrict__ fin,
+__global__ __launch_bounds__(64 * W) NOISE_WAVES_PER_EU(4) void k_rec_dec(const uint32_t *__restrict__ fin,
                                                      const SegRec *__restrict__ rt, RecHdr *hdr,
                                                      const uint8_t *in, uint8_t *out,
                                                      uint8_t *status) {
@@ -731,13 +738,19 @@ __global__ __launch_bounds__(64 * W) void k_rec_dec(const uint32_t *__restrict__
   const uint64_t nfin = hdr->counts[kClsLong], nlong = hdr->nlong;
   uint4 *lt = tile + 512u * wv;
   lds_u4 *lt3 = NOISE_LDS3(tile) + 512u * wv;
+  // thread 0 fetches the next record's index while the current one is
+  // decrypted (nxt, in a register until the loop top), so the atomic's round
+  // trip overlaps the Poly1305 pass's first loads
+  unsigned long long nxt = 0;
+  if (tid == 0) nxt = atomicAdd(&hdr->spare0, 1ull);
 #pragma unroll 1
   for (;;) {
-    if (tid == 0) item = atomicAdd(&hdr->spare0, 1ull);
+    if (tid == 0) item = nxt;
     __syncthreads();
     const uint64_t w = item;
     __syncthreads();  // every thread has read `item` before thread 0 rewrites it
     if (w >= nfin) break;
+    if (tid == 0) nxt = atomicAdd(&hdr->spare0, 1ull);
     const uint32_t q = fin[nfin - 1 - w];
     if (q >= nlong) continue;  // beyond the segment scratch: the generic kernel's
     const SegRec &R = rt[q];
@@ -879,7 +892,8 @@ __global__ __launch_bounds__(64 * W) void k_rec_dec(const uint32_t *__restrict__
     const uint4 want = (len & 15u) == 0 ? load16<true>(tp, 16) : load16<false>(tp, 16);
     const bool ok = ((want.x ^ tag[0]) | (want.y ^ tag[1]) | (want.z ^ tag[2]) |
                      (want.w ^ tag[3])) == 0u;
-    if (tid == 0) status[R.di] = ok ? NOISE_GPU_REC_OK : NOISE_GPU_REC_BAD_MAC;
+    // (the status byte is stored last: a store issued before the keystream
+    // pass would sit among the DMAs its counted waits expect)
 
     // ---- 3. plaintext ---------------------------------------------------
     if (!ok) {  // no plaintext leaves: in place untouched, a copy zeroed
@@ -891,6 +905,7 @@ __global__ __launch_bounds__(64 * W) void k_rec_dec(const uint32_t *__restrict__
           if (n >= 16u) store16<true>(dst + off, make_uint4(0u, 0u, 0u, 0u), 16);
           else store16<false>(dst + off, make_uint4(0u, 0u, 0u, 0u), (int)n);
         }
+      if (tid == 0) status[R.di] = NOISE_GPU_REC_BAD_MAC;
       continue;
     }
     uint32_t k[8];
@@ -902,12 +917,16 @@ __global__ __launch_bounds__(64 * W) void k_rec_dec(const uint32_t *__restrict__
 #pragma unroll 1
     for (uint32_t t = wv; t < ntile; t += W, buf ^= 1u) {
       // the next tile's DMA into the other buffer (its last reader, tile
-      // t - W's store loop, is done: lgkmcnt), then wait for all but it
+      // t - W's store loop, is done: lgkmcnt), then wait for this tile's DMA
+      // only: younger than it are tile t - W's 4 stores (a full tile issues
+      // exactly 4; then they stay in flight) and the next tile's 4 DMAs
       wait_lds();
       wave_lds_fence();
+      const bool prev_full = t != wv;  // tiles before the last are full
       if (t + W < ntile) {
         dma(t + W, buf ^ 1u);
-        wait_vmcnt<4>();
+        if (prev_full) wait_vmcnt<8>();
+        else wait_vmcnt<4>();
       } else {
         wait_vmem();
       }
@@ -940,6 +959,7 @@ __global__ __launch_bounds__(64 * W) void k_rec_dec(const uint32_t *__restrict__
         }
       }
     }
+    if (tid == 0) status[R.di] = NOISE_GPU_REC_OK;
   }
 }
 

@@ -7,7 +7,7 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT
 CFG=${1:-2}
 STEPS=${2:-20}
-O=$R/gpurun_out/prof_cfg$CFG
+O=${PROF_OUT:-$R/gpurun_out/prof_cfg$CFG}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 B="$R/bench.py --config $CFG --no-cpu-baseline --no-config1"

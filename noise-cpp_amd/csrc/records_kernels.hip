@@ -77,11 +77,13 @@ constexpr int kHdrWords = kSegChunks <= 4 ? 64 : 256;    // scratch header: 512 
 #ifndef NOISE_POLY_SPAN
 #define NOISE_POLY_SPAN 128
 #endif
-// Decrypt's long records: k_rec_dec with this many waves per record (1, 2,
-// 4), or 0 = the three-pass segment pipeline (kTileSegPoly, finalize,
-// kTileSegXor in kSegChunks chunks)
+// Decrypt's long records: 0 = the three-pass segment pipeline (kTileSegPoly,
+// finalize, kTileSegXor in kSegChunks chunks), or k_rec_dec with this many
+// waves per record (1, 2, 4).  Same box, config 4 (round 4,
+// profiles/round4/ab/cfg4_verify_first.md): decrypt 3.59-3.63 ms pipeline,
+// 4.63-4.69 k_rec_dec<1>, 4.79-4.86 k_rec_dec<2>.
 #ifndef NOISE_REC_DEC_W
-#define NOISE_REC_DEC_W 1
+#define NOISE_REC_DEC_W 0
 #endif
 #ifndef NOISE_CLASSIFY_MIN  // overridable for the CPU emulation build
 #define NOISE_CLASSIFY_MIN 2048

@@ -1242,6 +1242,14 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   const uint64_t gblocks = (nrec + kGenBlock - 1) / kGenBlock;
   const dim3 gg((unsigned)(gblocks < 2 * NOISE_GRID_CAP ? gblocks : 2 * NOISE_GRID_CAP));
   const dim3 gseg(capped((segbound + 63) / 64, NOISE_GRID_CAP));
+#ifndef NOISE_POLY_GRID  // A/B knobs: grid caps of the decrypt passes
+#define NOISE_POLY_GRID NOISE_GRID_CAP
+#endif
+#ifndef NOISE_XOR_GRID
+#define NOISE_XOR_GRID NOISE_GRID_CAP
+#endif
+  const dim3 gpoly(capped((segbound + 63) / 64, NOISE_POLY_GRID));
+  const dim3 gxor(capped((segbound + 63) / 64, NOISE_XOR_GRID));
   const dim3 gfin(capped((nrec + 64 / NOISE_FIN_W - 1) / (64 / NOISE_FIN_W), NOISE_GRID_CAP));
   RecHdr *hdr_w = const_cast<RecHdr *>(hdr);
 #define NOISE_DESC_TILES()                                                     \
@@ -1302,7 +1310,7 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   auto cidx = [chunks](int c) { return chunks > 1 ? c : -1; };
   for (int c = 0; c < chunks; ++c) {
     ac.chunk = cidx(c);
-    hipLaunchKernelGGL((k_aead_tile<true, 1024, false, kTileSegPoly, 0, 1, NOISE_POLY_SPAN>), gseg, bt, 0,
+    hipLaunchKernelGGL((k_aead_tile<true, 1024, false, kTileSegPoly, 0, 1, NOISE_POLY_SPAN>), gpoly, bt, 0,
                        stream, ac);
     if (c == 0 && (e = hipStreamWaitEvent(stream, ax.join, 0)) != hipSuccess) return e;
     hipLaunchKernelGGL((k_seg_finalize_w<true, NOISE_FIN_W>), gfin, bt, 0, stream, fin, rt, ta.partial,
@@ -1314,7 +1322,7 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   for (int c = 0; c < chunks; ++c) {
     ac.chunk = cidx(c);
     if ((e = hipStreamWaitEvent(ax.aux2, ax.fin[c], 0)) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_aead_tile<true, 1024, false, kTileSegXor, 0, 1, NOISE_XOR_SPAN>), gseg, bt, 0,
+    hipLaunchKernelGGL((k_aead_tile<true, 1024, false, kTileSegXor, 0, 1, NOISE_XOR_SPAN>), gxor, bt, 0,
                        ax.aux2, ac);
     if ((e = hipStreamWaitEvent(ax.aux, ax.fin[c], 0)) != hipSuccess) return e;
     hipLaunchKernelGGL((k_seg_tail<true, kTailXor>), grid, bt, 0, ax.aux, tails, rt, hdr, in, out,

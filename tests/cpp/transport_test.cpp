@@ -502,11 +502,13 @@ static int run_resident_probe(double cap_s) {
 }
 
 // A live resident instance for `secs` seconds (tools/gpu/r4_resident_cost.sh
-// runs the batch benches beside it): busy = 1 sends 1 KiB records back to
-// back, busy = 0 one record every 5 ms (the instance stays up, polling).
+// runs the batch benches beside it).  busy: 0 = a record every 5 ms, 1 = back
+// to back, 2 = one record, then the instance just polls; 3 = no instance, an
+// idle HIP context only (what a second process on the GPU costs by itself)
 static int run_resident_hold(double secs, int busy) {
   using clk = std::chrono::steady_clock;
-  if (noise_gpu_set_resident(1, 10000000) != NOISE_GPU_OK) return 1;
+  if (busy == 3 && hipFree(nullptr) != hipSuccess) return 1;
+  if (busy != 3 && noise_gpu_set_resident(1, 10000000) != NOISE_GPU_OK) return 1;
   std::array<std::uint8_t, 32> key{};
   key[0] = 9;
   bytes buf(1024 + 16);
@@ -514,11 +516,15 @@ static int run_resident_hold(double secs, int busy) {
   const auto t0 = clk::now();
   const char *stop_file = std::getenv("RESIDENT_HOLD_STOP");  // leave early once it exists
   while (std::chrono::duration<double>(clk::now() - t0).count() < secs) {
-    if (noise_gpu_encrypt_host(key.data(), (std::uint64_t)n, nullptr, 0, buf.data(), 1024) != NOISE_GPU_OK)
-      return 2;
-    ++n;
+    if (busy <= 1 || (busy == 2 && n == 0)) {
+      if (noise_gpu_encrypt_host(key.data(), (std::uint64_t)n, nullptr, 0, buf.data(), 1024) != NOISE_GPU_OK)
+        return 2;
+      ++n;
+    } else {
+      std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    }
     if (!busy) std::this_thread::sleep_for(std::chrono::milliseconds(5));
-    if (stop_file && (n & 255) == 0) {
+    if (stop_file && (busy >= 2 || (n & 255) == 0)) {
       if (FILE *f = std::fopen(stop_file, "r")) {
         std::fclose(f);
         break;
@@ -526,7 +532,8 @@ static int run_resident_hold(double secs, int busy) {
     }
   }
   const double t = std::chrono::duration<double>(clk::now() - t0).count();
-  (void)noise_gpu_set_resident(0, 0);
+  if (busy != 3) (void)noise_gpu_set_resident(0, 0);
+  if (n == 0) n = 1;
   std::printf("{\"resident_hold\": %d, \"records\": %ld, \"seconds\": %.2f, \"us_per_record\": %.3f}\n",
               busy, n, t, t / (double)n * 1e6);
   return 0;

@@ -21,72 +21,18 @@ JOBS = "-j%d" % max(1, min(8, os.cpu_count() or 1))  # the ASan objects build in
 BIN = os.path.join(EMU, "build", "emu_records")
 
 
-def _build(*extra):
-    r = subprocess.run(["make", JOBS, "-C", EMU, "GRID_CAP=3u", *extra], capture_output=True,
-                       text=True, timeout=900)
-    if r.returncode != 0:
-        pytest.fail("emulation build failed:\n" + r.stdout[-2000:] + r.stderr[-4000:])
-
-
-@pytest.fixture(scope="module")
-def emu_bin():
-    _build()
-    return BIN
-
-
-@pytest.fixture(scope="module")
-def emu_bin_small_cap():
-    _build("SEG_CAP=300ull")
-    return BIN + "_seg300ull"
-
-
-def _run(binary, mode, nrec, seed, gap):
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:allocator_may_return_null=1")
-    return subprocess.run([binary, mode, str(nrec), str(seed), str(gap)], capture_output=True,
-                          text=True, timeout=900, env=env)
-
-
-@pytest.mark.parametrize("mode,nrec,seed,gap", [
+# The emulated runs are independent processes that each keep about one core
+# busy (a block's threads take turns at the wave barriers), so the module
+# builds every binary once and then starts all runs together on a small pool;
+# each test waits for its own.  That keeps the CPU suite's wall time near the
+# longest single run instead of the sum.
+RECORDS_CASES = [
     ("cfg4", 700, 4, 0),
     ("cfg4", 2500, 8, 0),   # >= 1000 records (emulation build): the chunked decrypt pipeline
     ("inplace", 500, 5, (2 << 30) + 4096),
     ("ragged", 300, 6, 0),
-])
-def test_records_path_emulated(emu_bin, mode, nrec, seed, gap):
-    """...and verify-before-write (crypto_aead_read, monocypher.c:2912-2929):
-    every 16-byte store of the decrypt is watched (tools/emu store hook); no
-    store puts a non-zero byte into the output range of a record whose tag
-    fails, nor lands at all in one decrypted in place -- the segmented path
-    (>= 1 KiB records) included: its Poly1305 pass and the finalize check
-    every tag before the keystream pass writes any plaintext."""
-    r = _run(emu_bin, mode, nrec, seed, gap)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]
-    assert "ok (0 failures)" in r.stdout
-    assert ": 0 stores of unverified plaintext" in r.stdout
-    assert "watched 0 failed" not in r.stdout  # the batch holds tampered long records
-
-
-def test_host_entry_points_emulated_and_wiped():
-    """The C ABI's host-buffer entry points (noise_gpu_api.hip: the latency
-    kernel for single records, the staged lane walk for AD > 8 KiB, rekey, the
-    records path with its scratch, the uniform host pipeline) on the CPU under
-    AddressSanitizer, bit-exact against the oracle, and after EVERY call every
-    buffer the engine allocated is zero: no key, plaintext, ciphertext or
-    one-time key is left in staging or scratch (monocypher.c:163-167)."""
-    r = subprocess.run(["make", JOBS, "-C", EMU, "GRID_CAP=3u", "api"], capture_output=True, text=True,
-                       timeout=900)
-    if r.returncode != 0:
-        pytest.fail("emulation build failed:\n" + r.stdout[-2000:] + r.stderr[-4000:])
-    # leak detection on: noise_gpu_ctx_destroy and noise_gpu_thread_release
-    # must free everything the engine allocated (the run ends with both)
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1")
-    r = subprocess.run([os.path.join(EMU, "build", "emu_api")], capture_output=True, text=True,
-                       timeout=900, env=env)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]
-    assert "emu_api ok" in r.stdout
-
-
-@pytest.mark.parametrize("args", [
+]
+TRANSPORT_CASES = [
     ["pipeline", "10", "300", "2"],                       # launcher thread, tiny slots
     ["pipeline", "10", "300", "3"],                       # flush() issues its own work
     ["pipeline_batch", "20", "600", "4"],                 # copy pool, ragged batches
@@ -96,57 +42,124 @@ def test_host_entry_points_emulated_and_wiped():
     # 96 copy threads, 64 KiB slots of ~85 messages: the byte cut leaves fewer
     # messages than threads (empty chunks must keep their own index)
     ["pipeline_batch", "40", "4500", "8", "8192", str(64 << 10), "1500", "20000", "96", "0"],
-])
-def test_transport_pipeline_emulated(args):
+]
+BUILD = os.path.join(EMU, "build")
+ASAN_NOLEAK = "detect_leaks=0:allocator_may_return_null=1"
+
+
+def _make(*args):
+    r = subprocess.run(["make", JOBS, "-C", EMU, *args], capture_output=True, text=True, timeout=1200)
+    if r.returncode != 0:
+        pytest.fail("emulation build failed:\n" + r.stdout[-2000:] + r.stderr[-4000:])
+
+
+def _job_list():
+    jobs = {}
+    for mode, nrec, seed, gap in RECORDS_CASES:
+        jobs["records-%s-%d" % (mode, nrec)] = (
+            [BIN, mode, str(nrec), str(seed), str(gap)], ASAN_NOLEAK, 900)
+    jobs["records-overflow"] = ([BIN + "_seg300ull", "cfg4", "700", "7", "0"], ASAN_NOLEAK, 900)
+    # leak detection on: noise_gpu_ctx_destroy and noise_gpu_thread_release
+    # must free everything the engine allocated (the run ends with both)
+    jobs["api"] = ([os.path.join(BUILD, "emu_api")], "detect_leaks=1", 900)
+    for i, args in enumerate(TRANSPORT_CASES):
+        jobs["transport-%d" % i] = ([os.path.join(BUILD, "emu_transport"), *args], "detect_leaks=1", 600)
+    jobs["handshake"] = ([os.path.join(BUILD, "emu_handshake"),
+                          os.path.join(ROOT, "tests", "golden", "handshake_vectors.tsv")], "detect_leaks=0", 900)
+    jobs["x25519"] = ([os.path.join(BUILD, "emu_x25519"), "300", "11"], "detect_leaks=0", 300)
+    return jobs
+
+
+@pytest.fixture(scope="module")
+def emu():
+    """Build every emulation binary, start every run; name -> future of its
+    CompletedProcess (slowest first, so the pool drains evenly)."""
+    import concurrent.futures
+    _make("GRID_CAP=3u")
+    _make("GRID_CAP=3u", "SEG_CAP=300ull")
+    _make("GRID_CAP=3u", "api")
+    _make("GRID_CAP=3u", "transport")
+    _make("handshake")
+    jobs = _job_list()
+    order = ["transport-5", "api", "handshake", "records-ragged-300", "records-cfg4-2500"]
+    order += [k for k in jobs if k not in order]
+
+    def run(name):
+        argv, asan, timeout = jobs[name]
+        return subprocess.run(argv, capture_output=True, text=True, timeout=timeout,
+                              env=dict(os.environ, ASAN_OPTIONS=asan))
+    workers = max(2, min(6, (os.cpu_count() or 2) - 1))
+    pool = concurrent.futures.ThreadPoolExecutor(max_workers=workers)
+    futs = {name: pool.submit(run, name) for name in order}
+    yield futs
+    pool.shutdown(wait=True)
+
+
+def _result(emu, name):
+    return emu[name].result()
+
+
+@pytest.mark.parametrize("mode,nrec,seed,gap", RECORDS_CASES)
+def test_records_path_emulated(emu, mode, nrec, seed, gap):
+    """...and verify-before-write (crypto_aead_read, monocypher.c:2912-2929):
+    every 16-byte store of the decrypt is watched (tools/emu store hook); no
+    store puts a non-zero byte into the output range of a record whose tag
+    fails, nor lands at all in one decrypted in place -- the segmented path
+    (>= 1 KiB records) included: its Poly1305 pass and the finalize check
+    every tag before the keystream pass writes any plaintext."""
+    r = _result(emu, "records-%s-%d" % (mode, nrec))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]
+    assert "ok (0 failures)" in r.stdout
+    assert ": 0 stores of unverified plaintext" in r.stdout
+    assert "watched 0 failed" not in r.stdout  # the batch holds tampered long records
+
+
+def test_host_entry_points_emulated_and_wiped(emu):
+    """The C ABI's host-buffer entry points (noise_gpu_api.hip: the latency
+    kernel for single records, the staged lane walk for AD > 8 KiB, rekey, the
+    records path with its scratch, the uniform host pipeline) on the CPU under
+    AddressSanitizer, bit-exact against the oracle, and after EVERY call every
+    buffer the engine allocated is zero: no key, plaintext, ciphertext or
+    one-time key is left in staging or scratch (monocypher.c:163-167)."""
+    r = _result(emu, "api")
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]
+    assert "emu_api ok" in r.stdout
+
+
+@pytest.mark.parametrize("idx", range(len(TRANSPORT_CASES)))
+def test_transport_pipeline_emulated(emu, idx):
     """noise::transport::Pipeline (host/transport.cpp: copy pool, launcher
     thread, parallel submit_batch bookkeeping, key-table uploads) over the
     emulated C ABI, under AddressSanitizer with leak detection: ciphertexts vs
     the oracle, nonce accounting, tampered records, and every slot stream's
     records scratch and companion stream released with the Pipeline."""
-    r = subprocess.run(["make", JOBS, "-C", EMU, "GRID_CAP=3u", "transport"], capture_output=True,
-                       text=True, timeout=900)
-    if r.returncode != 0:
-        pytest.fail("emulation build failed:\n" + r.stdout[-2000:] + r.stderr[-4000:])
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1")
-    r = subprocess.run([os.path.join(EMU, "build", "emu_transport"), *args], capture_output=True,
-                       text=True, timeout=600, env=env)
+    r = _result(emu, "transport-%d" % idx)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]
     assert "ok (0 failures)" in r.stdout
 
 
-def test_records_segment_overflow_emulated(emu_bin_small_cap):
+def test_records_segment_overflow_emulated(emu):
     # long records past the 300-segment scratch fall back to the generic kernel
-    r = _run(emu_bin_small_cap, "cfg4", 700, 7, 0)
+    r = _result(emu, "records-overflow")
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]
     assert "ok (0 failures)" in r.stdout
 
 
-def test_emulated_batched_handshakes():
+def test_emulated_batched_handshakes(emu):
     """The batched-handshake kernels (csrc/handshake_kernels.hip) and their
     host driver (csrc/handshake_batch.hip), unmodified, on the CPU under ASan:
     the reference's 110 vectors through noise_gpu_hs_* -- messages, handshake
     hashes, split keys, transport records under them vs the oracle."""
-    r = subprocess.run(["make", JOBS, "-C", EMU, "handshake"], capture_output=True, text=True, timeout=900)
-    if r.returncode != 0:
-        pytest.fail("emulation build failed:\n" + r.stdout[-2000:] + r.stderr[-4000:])
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
-    r = subprocess.run([os.path.join(EMU, "build", "emu_handshake"),
-                        os.path.join(ROOT, "tests", "golden", "handshake_vectors.tsv")],
-                       capture_output=True, text=True, timeout=900, env=env)
+    r = _result(emu, "handshake")
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "vectors 110, failed 0" in r.stdout and "transport records 211" in r.stdout, r.stdout
 
 
-def test_emulated_fixed_base_public_keys():
+def test_emulated_fixed_base_public_keys(emu):
     """x25519_device.hpp's fixed-base path (edwards25519 radix-16 table,
     constant-time selects) on the CPU under ASan: RFC 7748 §6.1 and random /
     extreme scalars against the device ladder with u = 9 and the host X25519."""
-    r = subprocess.run(["make", JOBS, "-C", EMU, "handshake"], capture_output=True, text=True, timeout=900)
-    if r.returncode != 0:
-        pytest.fail("emulation build failed:\n" + r.stdout[-2000:] + r.stderr[-4000:])
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
-    r = subprocess.run([os.path.join(EMU, "build", "emu_x25519"), "300", "11"], capture_output=True,
-                       text=True, timeout=300, env=env)
+    r = _result(emu, "x25519")
     assert r.returncode == 0 and "0 failures: ok" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
 
 

@@ -77,14 +77,6 @@ constexpr int kHdrWords = kSegChunks <= 4 ? 64 : 256;    // scratch header: 512 
 #ifndef NOISE_POLY_SPAN
 #define NOISE_POLY_SPAN 128
 #endif
-// Decrypt's long records: 0 = the three-pass segment pipeline (kTileSegPoly,
-// finalize, kTileSegXor in kSegChunks chunks), or k_rec_dec with this many
-// waves per record (1, 2, 4).  Same box, config 4 (round 4,
-// profiles/round4/ab/cfg4_verify_first.md): decrypt 3.59-3.63 ms pipeline,
-// 4.63-4.69 k_rec_dec<1>, 4.79-4.86 k_rec_dec<2>.
-#ifndef NOISE_REC_DEC_W
-#define NOISE_REC_DEC_W 0
-#endif
 #ifndef NOISE_CLASSIFY_MIN  // overridable for the CPU emulation build
 #define NOISE_CLASSIFY_MIN 2048
 #endif
@@ -688,283 +680,6 @@ __global__ __launch_bounds__(64) void k_seg_finalize_w(
   }
 }
 
-// ---- decrypt: one workgroup per long record ---------------------------------
-// k_rec_dec<W>: W waves take one long record at a time (a work counter over
-// the classifier's segment-count buckets, largest records first) and decrypt
-// it whole, checking the tag before any plaintext is stored
-// (crypto_aead_read, monocypher.c:2912-2929):
-//   1. Poly1305: the workgroup's T = 64 W lanes read the ciphertext in
-//      coalesced steps of T 16-byte blocks; lane t keeps the Horner sum, in
-//      R = r^T, of blocks t, t + T, t + 2T, ...  The record's N = nb + 1
-//      blocks (nb ciphertext blocks, the last zero padded, then the length
-//      block) are front-padded to a multiple of T with zero blocks (no 2^128
-//      bit: they add nothing), so lane t's sum carries the weight r^(T - t):
-//      a 6-level butterfly in r, r^2, .., r^32 per wave, times r, then
-//      r^(64 (W - 1 - wave)) across the waves through LDS;
-//   2. the tag check (status per descriptor);
-//   3. keystream, verified records only: wave w takes the 4 KiB tiles w,
-//      w + W, ...: LDS-DMA in, lane L XORs ChaCha block 1 + 64 tile + L into
-//      its 64 bytes in place, the plaintext leaves in 16-byte pieces.  A
-//      failed record is left alone in place and zeroed out of place.
-// The second read of a record's ciphertext follows the first by about one
-// record's time, so the caches serve much of it, and there are no segment
-// partial sums, no finalize and no tail kernels on this path.
-// LDS slot s of a tile holds 16-byte piece rswz(s) (an involution): lane L's
-// ds_read/ds_write_b128 of pieces 4L..4L+3 and the lane-linear store reads
-// are all bank-conflict free on gfx950 (16-lane read groups over 16 slots,
-// 8-lane write groups over 8).
-__device__ __forceinline__ uint32_t rswz(uint32_t s) {
-  return s ^ (((s >> 4) & 1u) | ((((s >> 3) ^ (s >> 5)) & 1u) << 1));
-}
-
-#if defined(NOISE_HIP_EMU)
-#define NOISE_WAVES_PER_EU(n)
-#else
-#define NOISE_WAVES_PER_EU(n) __attribute__((amdgpu_waves_per_eu(n)))
-#endif
-// 4 waves per SIMD (<= 128 VGPRs): the Poly1305 pass waits on its loads,
-// and other waves' keystream work fills those waits
-template <int W>
-__global__ __launch_bounds__(64 * W) NOISE_WAVES_PER_EU(4) void k_rec_dec(const uint32_t *__restrict__ fin,
-                                                     const SegRec *__restrict__ rt, RecHdr *hdr,
-                                                     const uint8_t *in, uint8_t *out,
-                                                     uint8_t *status) {
-  static_assert(W == 1 || W == 2 || W == 4, "1, 2 or 4 waves per record");
-  constexpr uint32_t T = 64u * W;
-  __shared__ uint4 tile[W * 512];  // per wave: two 4 KiB keystream tiles
-  __shared__ uint32_t red[W * 5];
-  __shared__ unsigned long long item;
-  // wv through readfirstlane: the wave's LDS tile address is then an SGPR
-  // value (the LDS-DMA takes it in M0)
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = uniform32(tid >> 6);
-  const uint64_t nfin = hdr->counts[kClsLong], nlong = hdr->nlong;
-  uint4 *lt = tile + 512u * wv;
-  lds_u4 *lt3 = NOISE_LDS3(tile) + 512u * wv;
-  // thread 0 fetches the next record's index while the current one is
-  // decrypted (nxt, in a register until the loop top), so the atomic's round
-  // trip overlaps the Poly1305 pass's first loads
-  unsigned long long nxt = 0;
-  if (tid == 0) nxt = atomicAdd(&hdr->spare0, 1ull);
-#pragma unroll 1
-  for (;;) {
-    if (tid == 0) item = nxt;
-    __syncthreads();
-    const uint64_t w = item;
-    __syncthreads();  // every thread has read `item` before thread 0 rewrites it
-    if (w >= nfin) break;
-    if (tid == 0) nxt = atomicAdd(&hdr->spare0, 1ull);
-    const uint32_t q = fin[nfin - 1 - w];
-    if (q >= nlong) continue;  // beyond the segment scratch: the generic kernel's
-    const SegRec &R = rt[q];
-    const uint32_t len = R.len;
-    const uint32_t nb = (len + 15u) >> 4, N = nb + 1u;
-    const uint32_t C = (N + T - 1u) / T, pad = C * T - N;
-    const uint8_t *src = in + R.in_off;
-    uint8_t *dst = out + R.out_off;
-
-    // ---- 1. Poly1305 ------------------------------------------------------
-    F26 pw[6], r64, Rs;
-    pw[0] = to26(R.r[0], R.r[1], R.r[2], R.r[3], 0u);
-    pw[1] = mul26(pw[0], pw[0]);
-    pw[2] = mul26(pw[1], pw[1]);
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-      pw[3].a[i] = R.pw8[i];
-      pw[4].a[i] = R.pw16[i];
-      pw[5].a[i] = R.pw32[i];
-      r64.a[i] = R.r64[i];
-    }
-    Rs = r64;
-    if (W >= 2) Rs = mul26(Rs, Rs);  // r^128
-    const F26 r128 = Rs;
-    if (W == 4) Rs = mul26(Rs, Rs);  // r^256
-    F26 acc;
-#pragma unroll
-    for (int i = 0; i < 5; ++i) acc.a[i] = 0u;
-    const int64_t i0 = (int64_t)tid - (int64_t)pad;
-    // lane's block of step c: a ciphertext block, the length block, or a
-    // front-pad zero (hib 0: no 2^128 bit)
-    auto blk = [&](uint32_t c, uint4 &m, uint32_t &hib) {
-      const int64_t i = i0 + (int64_t)c * T;
-      m = make_uint4(0u, 0u, 0u, 0u);
-      hib = 0u;
-      if (c < C) {
-        if (i >= 0 && i < (int64_t)nb) {
-          const u32x4 v = *(const g_u32x4 *)(src + 16 * i);
-          m = make_uint4(v.x, v.y, v.z, v.w);
-          hib = 1u;
-        } else if (i == (int64_t)nb) {  // LE64(ad_len = 0) || LE64(len)
-          m = make_uint4(0u, 0u, len, 0u);
-          hib = 1u;
-        }
-      }
-    };
-    // two batches of kB steps in flight: batch b + 1's loads go out before
-    // batch b's products
-    constexpr uint32_t kB = 4;
-    uint4 ma[kB], mb[kB];
-    uint32_t ha[kB], hb[kB];
-#pragma unroll
-    for (uint32_t u = 0; u < kB; ++u) blk(u, ma[u], ha[u]);
-#pragma unroll 1
-    for (uint32_t c0 = 0; c0 < C; c0 += kB) {
-#pragma unroll
-      for (uint32_t u = 0; u < kB; ++u) blk(c0 + kB + u, mb[u], hb[u]);
-#pragma unroll
-      for (uint32_t u = 0; u < kB; ++u) {
-        if (c0 + u >= C) break;
-        const int64_t i = i0 + (int64_t)(c0 + u) * T;
-        uint4 m = ma[u];
-        if (i == (int64_t)nb - 1 && (len & 15u)) m = mask_bytes(m, (int)(len & 15u));
-        acc = mul26(acc, Rs);
-        const F26 x = to26(m.x, m.y, m.z, m.w, ha[u]);
-#pragma unroll
-        for (int k = 0; k < 5; ++k) acc.a[k] += x.a[k];
-      }
-#pragma unroll
-      for (uint32_t u = 0; u < kB; ++u) {
-        ma[u] = mb[u];
-        ha[u] = hb[u];
-      }
-    }
-    // The keystream pass's first tile now (a load: nothing of the record is
-    // stored before its tag is checked), so it lands during the sums below.
-    // Every tile DMA issues all 4 instructions (pieces past the record read
-    // its last one instead) so that the counted waits below stay exact.
-    const uint32_t ntile = (len + 4095u) >> 12, lastp = 16u * (nb - 1u);
-    const uint64_t ga = (uint64_t)(uintptr_t)src;
-    const uint8_t *gsrc = (const uint8_t *)(uintptr_t)join64(uniform32((uint32_t)(ga >> 32)),
-                                                             uniform32((uint32_t)ga));
-    auto dma = [&](uint32_t t, uint32_t buf) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t off = (t << 12) + 16u * rswz(64u * j + lane);
-        lds_dma16_s(gsrc, off < len ? off : lastp, (lds_void *)(lt3 + 256u * buf + 64u * j));
-      }
-    };
-    wait_lds();  // the previous record's last LDS reads are done
-    wave_lds_fence();
-    if (wv < ntile) dma(wv, 0u);
-
-    // sum over the wave's lanes: S = sum_L acc_L r^(63 - L), then times r
-    F26 S = acc;
-#pragma unroll
-    for (int b = 0; b < 6; ++b) {
-      const bool lower = ((lane >> b) & 1u) == 0u;
-      F26 lo, up;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        const uint32_t o = (uint32_t)__shfl_xor((int)S.a[k], 1 << b);
-        lo.a[k] = lower ? S.a[k] : o;
-        up.a[k] = lower ? o : S.a[k];
-      }
-      S = mul26(lo, pw[b]);
-#pragma unroll
-      for (int k = 0; k < 5; ++k) S.a[k] += up.a[k];
-      carry26(S);
-    }
-    S = mul26(S, pw[0]);
-    if (W > 1) {  // wave wv's sum weighs r^(64 (W - 1 - wv))
-      const uint32_t e = W - 1u - wv;
-      if (e >= 2u) S = mul26(S, r128);
-      if (e & 1u) S = mul26(S, r64);
-      if (lane == 0) {
-#pragma unroll
-        for (int k = 0; k < 5; ++k) red[5 * wv + k] = S.a[k];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        uint32_t v = 0u;
-#pragma unroll
-        for (int x = 0; x < W; ++x) v += red[5 * x + k];
-        S.a[k] = v;
-      }
-    }
-    carry26(S);
-    carry26(S);
-    Poly1305 p;
-    from26(S, p.h0, p.h1, p.h2, p.h3, p.h4);
-    p.s0 = R.s[0]; p.s1 = R.s[1]; p.s2 = R.s[2]; p.s3 = R.s[3];
-    uint32_t tag[4];
-    poly_final(p, tag);
-
-    // ---- 2. the tag -----------------------------------------------------
-    const uint8_t *tp = src + len;
-    const uint4 want = (len & 15u) == 0 ? load16<true>(tp, 16) : load16<false>(tp, 16);
-    const bool ok = ((want.x ^ tag[0]) | (want.y ^ tag[1]) | (want.z ^ tag[2]) |
-                     (want.w ^ tag[3])) == 0u;
-    // (the status byte is stored last: a store issued before the keystream
-    // pass would sit among the DMAs its counted waits expect)
-
-    // ---- 3. plaintext ---------------------------------------------------
-    if (!ok) {  // no plaintext leaves: in place untouched, a copy zeroed
-      wait_vmem();  // the prefetched tile has landed before its buffer is reused
-      if (src != dst)
-#pragma unroll 1
-        for (uint32_t off = 16u * tid; off < len; off += 16u * T) {
-          const uint32_t n = len - off;
-          if (n >= 16u) store16<true>(dst + off, make_uint4(0u, 0u, 0u, 0u), 16);
-          else store16<false>(dst + off, make_uint4(0u, 0u, 0u, 0u), (int)n);
-        }
-      if (tid == 0) status[R.di] = NOISE_GPU_REC_BAD_MAC;
-      continue;
-    }
-    uint32_t k[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) k[i] = R.k[i];
-    const uint32_t n_lo = (uint32_t)R.nonce, n_hi = (uint32_t)(R.nonce >> 32);
-    const ChaPre pre = chacha_pre(k, n_lo, n_hi);
-    uint32_t buf = 0u;
-#pragma unroll 1
-    for (uint32_t t = wv; t < ntile; t += W, buf ^= 1u) {
-      // the next tile's DMA into the other buffer (its last reader, tile
-      // t - W's store loop, is done: lgkmcnt), then wait for this tile's DMA
-      // only: younger than it are tile t - W's 4 stores (a full tile issues
-      // exactly 4; then they stay in flight) and the next tile's 4 DMAs
-      wait_lds();
-      wave_lds_fence();
-      const bool prev_full = t != wv;  // tiles before the last are full
-      if (t + W < ntile) {
-        dma(t + W, buf ^ 1u);
-        if (prev_full) wait_vmcnt<8>();
-        else wait_vmcnt<4>();
-      } else {
-        wait_vmem();
-      }
-      wave_lds_fence();
-      uint4 *lb = lt + 256u * buf;
-      const uint32_t base = t << 12;
-      if (base + 64u * lane < len) {
-        uint32_t ks[16];
-        chacha20_block_pre(k, 1u + (base >> 6) + lane, pre, n_lo, n_hi, ks);
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          const uint32_t slot = rswz(4u * lane + kk);
-          uint4 v = lb[slot];
-          v.x ^= ks[4 * kk + 0];
-          v.y ^= ks[4 * kk + 1];
-          v.z ^= ks[4 * kk + 2];
-          v.w ^= ks[4 * kk + 3];
-          lb[slot] = v;
-        }
-      }
-      wave_lds_fence();
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t pc = 64u * j + lane, off = base + 16u * pc;
-        if (off < len) {
-          const uint4 v = lb[rswz(pc)];
-          const uint32_t n = len - off;
-          if (n >= 16u) store16<true>(dst + off, v, 16);
-          else store16<false>(dst + off, v, (int)n);
-        }
-      }
-    }
-    if (tid == 0) status[R.di] = NOISE_GPU_REC_OK;
-  }
-}
-
 // ---- generic: one lane per record ------------------------------------------
 // idx == nullptr: record i directly (small batches).  Otherwise the generic
 // class, followed by the long records the segment scratch could not take.
@@ -1278,23 +993,8 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
                        ta.partial_hi, hdr_w, in, out, status, -1);
     return hipGetLastError();
   }
-#if NOISE_REC_DEC_W > 0
-  // decrypt: the long records whole, one workgroup each (k_rec_dec), beside
-  // the companion's small classes and generic kernel
-  NOISE_DESC_TILES()
-  if ((e = hipEventRecord(ax.join, ax.aux)) != hipSuccess) return e;
-  {
-    constexpr unsigned kW = NOISE_REC_DEC_W;
-    const dim3 grec(capped(nrec, NOISE_GRID_CAP / kW > 0 ? NOISE_GRID_CAP / kW : 1));
-    hipLaunchKernelGGL((k_rec_dec<kW>), grec, dim3(64 * kW), 0, stream, fin, rt, hdr_w, in, out, status);
-  }
-  if ((e = hipStreamWaitEvent(stream, ax.join, 0)) != hipSuccess) return e;
-  (void)chunks;
-  return hipGetLastError();
-#endif
-  // decrypt (NOISE_REC_DEC_W=0: the segment pipeline).  Companion: the tails'
-  // Poly1305 first (the first tag check waits for it), then the small classes
-  // and the generic kernel
+  // decrypt.  Companion: the tails' Poly1305 first (the first tag check
+  // waits for it), then the small classes and the generic kernel
   if ((e = hipStreamWaitEvent(ax.aux, ax.prep, 0)) != hipSuccess) return e;
   hipLaunchKernelGGL((k_seg_tail<true, kTailPoly>), grid, bt, 0, ax.aux, tails, rt, hdr, in, out, -1);
   if ((e = hipEventRecord(ax.join, ax.aux)) != hipSuccess) return e;

@@ -833,14 +833,11 @@ static inline unsigned capped(uint64_t want, uint64_t cap) {
 struct AuxStream {
   hipStream_t aux = nullptr;   // companion: small classes, generic, tails
   hipStream_t aux2 = nullptr;  // decrypt: per chunk, tag check + plaintext pass
-  hipStream_t aux3 = nullptr;  // decrypt: small classes, generic (join3)
   // fork: classifier done; prep: k_seg_prep done; join: encrypt: the
   // companion branch done, decrypt: the tails' Poly1305 done; join2: the
-  // companion done (decrypt); join3: companion 3 done (decrypt); xdone: the
-  // last plaintext pass done; poly[c] / fin[c]: chunk c's Poly1305 pass / tag
-  // check done
-  hipEvent_t fork = nullptr, prep = nullptr, join = nullptr, join2 = nullptr, xdone = nullptr,
-             join3 = nullptr;
+  // companion done (decrypt); xdone: the last plaintext pass done; poly[c] /
+  // fin[c]: chunk c's Poly1305 pass / tag check done
+  hipEvent_t fork = nullptr, prep = nullptr, join = nullptr, join2 = nullptr, xdone = nullptr;
   hipEvent_t poly[kSegChunks] = {}, fin[kSegChunks] = {};
 };
 struct AuxEntry {
@@ -866,8 +863,7 @@ static hipError_t aux_get(AuxStream *out, hipStream_t stream) {
   AuxStream a;
   if ((e = hipStreamCreateWithFlags(&a.aux, hipStreamNonBlocking)) != hipSuccess) return e;
   if ((e = hipStreamCreateWithFlags(&a.aux2, hipStreamNonBlocking)) != hipSuccess) return e;
-  if ((e = hipStreamCreateWithFlags(&a.aux3, hipStreamNonBlocking)) != hipSuccess) return e;
-  for (hipEvent_t *ev : {&a.fork, &a.join, &a.prep, &a.join2, &a.xdone, &a.join3})
+  for (hipEvent_t *ev : {&a.fork, &a.join, &a.prep, &a.join2, &a.xdone})
     if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return e;
   for (int c = 0; c < kSegChunks; ++c)
     for (hipEvent_t *ev : {&a.poly[c], &a.fin[c]})
@@ -892,13 +888,13 @@ static hipError_t aux_release(int dev, hipStream_t stream) {
   }
   if (!found) return hipSuccess;
   hipError_t e = hipSuccess, e2;
-  for (hipStream_t st : {a.aux, a.aux2, a.aux3}) {
+  for (hipStream_t st : {a.aux, a.aux2}) {
     e2 = hipStreamSynchronize(st);
     if (e == hipSuccess) e = e2;
     e2 = hipStreamDestroy(st);
     if (e == hipSuccess) e = e2;
   }
-  for (hipEvent_t ev : {a.fork, a.prep, a.join, a.join2, a.xdone, a.join3}) {
+  for (hipEvent_t ev : {a.fork, a.prep, a.join, a.join2, a.xdone}) {
     e2 = hipEventDestroy(ev);
     if (e == hipSuccess) e = e2;
   }
@@ -929,11 +925,10 @@ static hipError_t aux_release(int dev, hipStream_t stream) {
 // kSegChunks chunks and the Poly1305 pass of chunk c + 1 runs beside the
 // tag check and keystream pass of chunk c:
 //   caller     : prep -> Poly(0) -(wait join)-> check(0) -> Poly(1) -> check(1) -> ...
-//                ... -> check(K-1)                            (wait xdone, join2, join3)
-//   companion  : (wait prep) tail Poly1305 -> join,
+//                ... -> check(K-1)                                   (wait xdone, join2)
+//   companion  : (wait prep) tail Poly1305 -> join, small classes, generic,
 //                then per chunk (wait fin[c]) the chunk's tail plaintext -> join2
 //   companion 2: per chunk (wait fin[c]) XOR(c) -> xdone
-//   companion 3: (wait fork) small classes, generic -> join3
 template <bool DECRYPT>
 static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr *hdr,
                                  const uint8_t *keys, uint32_t nkeys,
@@ -948,7 +943,6 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
 #ifdef NOISE_RECORDS_SERIAL  // diagnostics only: every kernel on the caller's stream
   ax.aux = stream;
   ax.aux2 = stream;
-  ax.aux3 = stream;
 #endif
   const dim3 bt(64);
   const dim3 grid(capped((nrec + 63) / 64, NOISE_GRID_CAP));
@@ -973,7 +967,6 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   const dim3 gxor(capped((segbound + 63) / 64, NOISE_XOR_GRID));
   const dim3 gfin(capped((nrec + 64 / NOISE_FIN_W - 1) / (64 / NOISE_FIN_W), NOISE_GRID_CAP));
   RecHdr *hdr_w = const_cast<RecHdr *>(hdr);
-  hipStream_t cs = ax.aux;  // the small classes' and generic kernel's stream
 #define NOISE_DESC_TILES()                                                     \
   NOISE_DESC_TILE(0, 64)                                                       \
   NOISE_DESC_TILE(1, 128)                                                      \
@@ -981,11 +974,11 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   NOISE_DESC_TILE(3, 256)                                                      \
   NOISE_DESC_TILE(4, 512)                                                      \
   NOISE_DESC_TILE(5, 1024)                                                     \
-  hipLaunchKernelGGL((k_aead_records<DECRYPT>), gg, dim3(kGenBlock), 0, cs, keys, nkeys, recs,      \
+  hipLaunchKernelGGL((k_aead_records<DECRYPT>), gg, dim3(kGenBlock), 0, ax.aux, keys, nkeys, recs,  \
                      nrec, idx, hdr, in, out, ad, status);
 #define NOISE_DESC_TILE(C, LEN)                                                \
   a.cls = C;                                                                   \
-  hipLaunchKernelGGL((k_aead_tile<DECRYPT, LEN, false, kTileDesc>), grid, bt, 0, cs, a);
+  hipLaunchKernelGGL((k_aead_tile<DECRYPT, LEN, false, kTileDesc>), grid, bt, 0, ax.aux, a);
   if (!DECRYPT) {
     // companion: dense tile classes first, the long-latency tails last (they
     // then overlap the segment kernel's drain; tails first: -3..5 %)
@@ -1000,27 +993,12 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
                        ta.partial_hi, hdr_w, in, out, status, -1);
     return hipGetLastError();
   }
-  // decrypt.  Companion 3: the small classes and the generic kernel, from
-  // the classifier on.  Companion: the tails' Poly1305 (the first tag check
-  // waits for it), later each chunk's tail plaintext -- not queued behind the
-  // small classes, so the last tails are done with the last keystream pass
-  // (NOISE_DEC_AUX3=0: the small classes on the companion after the tails'
-  // Poly1305, as in the first round-4 build)
-#ifndef NOISE_DEC_AUX3
-#define NOISE_DEC_AUX3 1
-#endif
-  if (NOISE_DEC_AUX3) {
-    if ((e = hipStreamWaitEvent(ax.aux3, ax.fork, 0)) != hipSuccess) return e;
-    cs = ax.aux3;
-    NOISE_DESC_TILES()
-    if ((e = hipEventRecord(ax.join3, ax.aux3)) != hipSuccess) return e;
-  }
+  // decrypt.  Companion: the tails' Poly1305 first (the first tag check
+  // waits for it), then the small classes and the generic kernel
   if ((e = hipStreamWaitEvent(ax.aux, ax.prep, 0)) != hipSuccess) return e;
   hipLaunchKernelGGL((k_seg_tail<true, kTailPoly>), grid, bt, 0, ax.aux, tails, rt, hdr, in, out, -1);
   if ((e = hipEventRecord(ax.join, ax.aux)) != hipSuccess) return e;
-  if (!NOISE_DEC_AUX3) {
-    NOISE_DESC_TILES()
-  }
+  NOISE_DESC_TILES()
   // caller: per chunk, the Poly1305 pass and the tag check (the first one
   // also waits for the tails' P_tail).  The checks sit here, not in front of
   // the keystream passes, so chunk c + 1's is done while chunk c's plaintext
@@ -1056,7 +1034,6 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   if ((e = hipEventRecord(ax.join2, ax.aux)) != hipSuccess) return e;
   if ((e = hipStreamWaitEvent(stream, ax.xdone, 0)) != hipSuccess) return e;
   if ((e = hipStreamWaitEvent(stream, ax.join2, 0)) != hipSuccess) return e;
-  if (NOISE_DEC_AUX3 && (e = hipStreamWaitEvent(stream, ax.join3, 0)) != hipSuccess) return e;
   return hipGetLastError();
 }
 

@@ -96,6 +96,16 @@ constexpr uint64_t kSegCapMax = NOISE_SEG_CAP;  // 16 Mi segments = 16 GiB per c
 #define NOISE_GRID_CAP 8192u
 #endif
 
+// Grid caps of the decrypt passes (A/B knobs; round 4: capping the keystream
+// pass at 3072 waves cost 12 %, the Poly1305 pass at 2048 nothing --
+// profiles/round4/ab/cfg4_verify_first.md section 6)
+#ifndef NOISE_POLY_GRID
+#define NOISE_POLY_GRID NOISE_GRID_CAP
+#endif
+#ifndef NOISE_XOR_GRID
+#define NOISE_XOR_GRID NOISE_GRID_CAP
+#endif
+
 // an all-zero key row is "no key" (Noise HasKey() false, e.g. the rows
 // noise_gpu_hs_split leaves for failed handshakes): never used to encrypt
 __device__ __forceinline__ bool key_row_zero(const uint8_t *keys, uint32_t ki) {
@@ -957,12 +967,6 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   const uint64_t gblocks = (nrec + kGenBlock - 1) / kGenBlock;
   const dim3 gg((unsigned)(gblocks < 2 * NOISE_GRID_CAP ? gblocks : 2 * NOISE_GRID_CAP));
   const dim3 gseg(capped((segbound + 63) / 64, NOISE_GRID_CAP));
-#ifndef NOISE_POLY_GRID  // A/B knobs: grid caps of the decrypt passes
-#define NOISE_POLY_GRID NOISE_GRID_CAP
-#endif
-#ifndef NOISE_XOR_GRID
-#define NOISE_XOR_GRID NOISE_GRID_CAP
-#endif
   const dim3 gpoly(capped((segbound + 63) / 64, NOISE_POLY_GRID));
   const dim3 gxor(capped((segbound + 63) / 64, NOISE_XOR_GRID));
   const dim3 gfin(capped((nrec + 64 / NOISE_FIN_W - 1) / (64 / NOISE_FIN_W), NOISE_GRID_CAP));

@@ -373,10 +373,16 @@ typedef __attribute__((address_space(1))) u32x4 g_u32x4;
 typedef __attribute__((address_space(3))) void lds_void;
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
+// NOISE_DMA_NT: the streaming (nt) cache policy on the record DMAs (A/B knob)
+#if defined(NOISE_DMA_NT)
+#define NOISE_DMA_POLICY " nt"
+#else
+#define NOISE_DMA_POLICY ""
+#endif
 __device__ __forceinline__ void lds_dma16_s(const void *sbase, uint32_t voff,
                                             lds_void *lds_base) {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(NOISE_DMA_BUILTIN)
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" NOISE_DMA_POLICY
                :: "v"(voff), "s"(sbase), "s"((uint32_t)(uintptr_t)lds_base) : "memory", "m0");
 #else
   __builtin_amdgcn_global_load_lds((const void *)((const uint8_t *)sbase + voff), lds_base, 16, 0, 0);
@@ -384,7 +390,7 @@ __device__ __forceinline__ void lds_dma16_s(const void *sbase, uint32_t voff,
 }
 __device__ __forceinline__ void lds_dma16_v(const void *vaddr, lds_void *lds_base) {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(NOISE_DMA_BUILTIN)
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" NOISE_DMA_POLICY
                :: "v"(vaddr), "s"((uint32_t)(uintptr_t)lds_base) : "memory", "m0");
 #else
   __builtin_amdgcn_global_load_lds(vaddr, lds_base, 16, 0, 0);

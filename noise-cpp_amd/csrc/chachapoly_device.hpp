@@ -373,11 +373,14 @@ typedef __attribute__((address_space(1))) u32x4 g_u32x4;
 typedef __attribute__((address_space(3))) void lds_void;
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
-// NOISE_DMA_NT: the streaming (nt) cache policy on the record DMAs (A/B knob)
-#if defined(NOISE_DMA_NT)
-#define NOISE_DMA_POLICY " nt"
-#else
+// The record DMAs stream (nt: each byte is read once).  Same box, six
+// alternating runs each (round 4, profiles/round4/ab/dma_nt.md): config 2
+// +0.0..+2.3 %, config 4 +0.9..+2.6 %, every run faster.  NOISE_DMA_PLAIN
+// restores the default policy.
+#if defined(NOISE_DMA_PLAIN)
 #define NOISE_DMA_POLICY ""
+#else
+#define NOISE_DMA_POLICY " nt"
 #endif
 __device__ __forceinline__ void lds_dma16_s(const void *sbase, uint32_t voff,
                                             lds_void *lds_base) {

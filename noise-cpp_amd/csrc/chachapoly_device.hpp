@@ -448,11 +448,7 @@ __device__ __forceinline__ void store16(uint8_t *p, uint4 v, int n) {
     // one aligned global_store_dwordx4 (a plain uint4 store may be
     // re-split by the store merger into misaligned dwordx3/x4 pieces)
     const u32x4 w = {v.x, v.y, v.z, v.w};
-#if defined(NOISE_STORE_SC) && defined(__HIP_DEVICE_COMPILE__)  // A/B knob: sc0 sc1 policy
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"(p), "v"(w) : "memory");
-#else
     __builtin_nontemporal_store(w, (g_u32x4 *)p);
-#endif
     return;
   }
   st_bytes(p, v.x, n >= 4 ? 4 : n);

@@ -379,6 +379,10 @@ typedef __attribute__((address_space(3))) void lds_void;
 // restores the default policy.
 #if defined(NOISE_DMA_PLAIN)
 #define NOISE_DMA_POLICY ""
+#elif defined(NOISE_DMA_SC1)  // A/B knobs
+#define NOISE_DMA_POLICY " sc1 nt"
+#elif defined(NOISE_DMA_SC01)
+#define NOISE_DMA_POLICY " sc0 sc1 nt"
 #else
 #define NOISE_DMA_POLICY " nt"
 #endif

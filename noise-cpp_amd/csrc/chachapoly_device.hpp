@@ -375,14 +375,10 @@ typedef __attribute__((address_space(3))) void lds_void;
 #pragma clang diagnostic ignored "-Winline-asm"
 // The record DMAs stream (nt: each byte is read once).  Same box, six
 // alternating runs each (round 4, profiles/round4/ab/dma_nt.md): config 2
-// +0.0..+2.3 %, config 4 +0.9..+2.6 %, every run faster.  NOISE_DMA_PLAIN
-// restores the default policy.
+// +0.0..+2.3 %, config 4 +0.9..+2.6 %, every run faster; "sc1 nt" and
+// "sc0 sc1 nt" were no better.  NOISE_DMA_PLAIN restores the default policy.
 #if defined(NOISE_DMA_PLAIN)
 #define NOISE_DMA_POLICY ""
-#elif defined(NOISE_DMA_SC1)  // A/B knobs
-#define NOISE_DMA_POLICY " sc1 nt"
-#elif defined(NOISE_DMA_SC01)
-#define NOISE_DMA_POLICY " sc0 sc1 nt"
 #else
 #define NOISE_DMA_POLICY " nt"
 #endif

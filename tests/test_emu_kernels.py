@@ -81,16 +81,26 @@ def emu():
     _make("GRID_CAP=3u", "transport")
     _make("handshake")
     jobs = _job_list()
-    order = ["transport-5", "api", "handshake", "records-ragged-300", "records-cfg4-2500"]
-    order += [k for k in jobs if k not in order]
 
     def run(name):
         argv, asan, timeout = jobs[name]
         return subprocess.run(argv, capture_output=True, text=True, timeout=timeout,
                               env=dict(os.environ, ASAN_OPTIONS=asan))
+    # emu_api runs the resident latency kernel on a thread of its own with
+    # the host's timed waits around it: it runs alone, on an otherwise idle
+    # machine, as it always has (under the pool's load one run hit its time
+    # limit)
+    api = concurrent.futures.Future()
+    try:
+        api.set_result(run("api"))
+    except Exception as exc:  # noqa: BLE001 -- reported by the test
+        api.set_exception(exc)
+    order = ["transport-5", "handshake", "records-ragged-300", "records-cfg4-2500"]
+    order += [k for k in jobs if k not in order and k != "api"]
     workers = max(2, min(6, (os.cpu_count() or 2) - 1))
     pool = concurrent.futures.ThreadPoolExecutor(max_workers=workers)
     futs = {name: pool.submit(run, name) for name in order}
+    futs["api"] = api
     yield futs
     pool.shutdown(wait=True)
 

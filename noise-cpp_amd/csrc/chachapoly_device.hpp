@@ -373,28 +373,34 @@ typedef __attribute__((address_space(1))) u32x4 g_u32x4;
 typedef __attribute__((address_space(3))) void lds_void;
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
-// The record DMAs stream (nt: each byte is read once).  Same box, six
-// alternating runs each (round 4, profiles/round4/ab/dma_nt.md): config 2
-// +0.0..+2.3 %, config 4 +0.9..+2.6 %, every run faster; "sc1 nt" and
-// "sc0 sc1 nt" were no better.  NOISE_DMA_PLAIN restores the default policy.
-#if defined(NOISE_DMA_PLAIN)
-#define NOISE_DMA_POLICY ""
-#else
-#define NOISE_DMA_POLICY " nt"
-#endif
+// The record DMAs stream (NT = true, the nt policy: each byte is read once).
+// Same box, six alternating runs each (round 4, profiles/round4/ab/dma_nt.md):
+// config 2 +0.0..+2.3 %, config 4 +0.9..+2.6 %, every run faster; "sc1 nt"
+// and "sc0 sc1 nt" were no better.  NT = false (default policy) is for data
+// that is read again soon after (tile_load's POLICY).
+template <bool NT = true>
 __device__ __forceinline__ void lds_dma16_s(const void *sbase, uint32_t voff,
                                             lds_void *lds_base) {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(NOISE_DMA_BUILTIN)
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" NOISE_DMA_POLICY
-               :: "v"(voff), "s"(sbase), "s"((uint32_t)(uintptr_t)lds_base) : "memory", "m0");
+  if constexpr (NT)
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 nt"
+                 :: "v"(voff), "s"(sbase), "s"((uint32_t)(uintptr_t)lds_base) : "memory", "m0");
+  else
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+                 :: "v"(voff), "s"(sbase), "s"((uint32_t)(uintptr_t)lds_base) : "memory", "m0");
 #else
   __builtin_amdgcn_global_load_lds((const void *)((const uint8_t *)sbase + voff), lds_base, 16, 0, 0);
 #endif
 }
+template <bool NT = true>
 __device__ __forceinline__ void lds_dma16_v(const void *vaddr, lds_void *lds_base) {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(NOISE_DMA_BUILTIN)
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" NOISE_DMA_POLICY
-               :: "v"(vaddr), "s"((uint32_t)(uintptr_t)lds_base) : "memory", "m0");
+  if constexpr (NT)
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt"
+                 :: "v"(vaddr), "s"((uint32_t)(uintptr_t)lds_base) : "memory", "m0");
+  else
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                 :: "v"(vaddr), "s"((uint32_t)(uintptr_t)lds_base) : "memory", "m0");
 #else
   __builtin_amdgcn_global_load_lds(vaddr, lds_base, 16, 0, 0);
 #endif

@@ -189,6 +189,9 @@ thread_local Staging *tl_stage = nullptr;
 // relaunched by the next one), on the stop word, and at teardown.
 constexpr uint32_t kResidentIdleDefaultUs = 20000;
 constexpr std::chrono::seconds kOneWaitLimit{10};
+// fresh instances launched for one request that all left without taking it
+// (each sees the complete request on its first poll) before the call fails
+constexpr uint32_t kResidentMaxRelaunch = 8;
 constexpr uint32_t kResidentIdleMaxUs = 10000000;
 struct OneCtx;
 // contexts whose resident kernel may be running (stopped at library unload;
@@ -202,6 +205,13 @@ std::vector<OneCtx *> &resident_list() {
   return *v;
 }
 void resident_track(OneCtx *c, bool on);
+}  // namespace
+#if defined(NOISE_HIP_EMU)
+namespace noise_amd {
+uint32_t emu_req_check_flip = 0;  // tools/emu/emu_api.cpp: corrupts the next request's check word
+}
+#endif
+namespace {
 constexpr uint32_t kOneAliveOff = 8;  // u32 in the done line: 1 while an instance runs
 
 // Where the resident kernel's request image lives (NOISE_GPU_RESIDENT_REQ,
@@ -391,44 +401,59 @@ struct OneCtx {
   // rather than spin for ever.
   // by_resident: the request went to the resident instance (else a launch on
   // `stream`, the launch path's)
+  //
+  // Every 64th spin checks the time limit FIRST, before anything that can
+  // `continue` the loop: the wait is bounded whatever the instance does.
+  // (Round 4 checked it only on spins = 1023 mod 1024, after the relaunch
+  // branch, which fires on spins = 63 mod 64 -- a superset: with the alive
+  // word 0 at each of those spins, e.g. an instance that leaves without
+  // taking the request, the limit was never reached.)  An instance that left
+  // (alive word 0) is relaunched; a request that kResidentMaxRelaunch fresh
+  // instances in a row did not take -- each one saw the complete request on
+  // its first poll, so the request itself is refused (a torn or corrupted
+  // request line: check word or seq) -- fails the call.  No instance runs
+  // then, so the context stays usable; one_record wipes the request image.
   int wait(uint32_t s, bool by_resident) {
     hipStream_t wst = by_resident ? rstream : stream;
     volatile uint32_t *done = reinterpret_cast<volatile uint32_t *>(h);
     const auto t0 = std::chrono::steady_clock::now();
+    uint32_t relaunches = 0;
     for (uint64_t spin = 0;; ++spin) {
       if (*done == s) return NOISE_GPU_OK;
+      if ((spin & 63u) != 63u) continue;
+      const auto waited = std::chrono::steady_clock::now() - t0;
+      if (waited > kOneWaitLimit) {
+        if (*done == s) return NOISE_GPU_OK;
+        if (by_resident) (void)stop_resident();  // bounded; marks the context wedged if it must
+        if (!wedged) g_last_error = "latency kernel gave no answer within 10 s";
+        return NOISE_GPU_E_HIP;
+      }
       // the instance left on its idle timer after its last poll (it clears
       // the alive word last, after any done word it wrote): relaunch now
       // instead of after the first stream query below
-      if (by_resident && (spin & 63u) == 63u && *alive() == 0u) {
+      if (by_resident && *alive() == 0u) {
         if (*done == s) return NOISE_GPU_OK;
+        if (++relaunches > kResidentMaxRelaunch) {
+          g_last_error = "resident latency kernel did not take the request (relaunched without progress)";
+          return NOISE_GPU_E_HIP;
+        }
         const int rc = launch_resident(s - 1u);
         if (rc) return rc;
         continue;
       }
-      if ((spin & 1023u) == 1023u) {  // now and then: has the stream failed or ended?
-        const auto waited = std::chrono::steady_clock::now() - t0;
-        // a record takes microseconds: the stream query (a runtime call of
-        // ~1 us) is for the rare stall, not for every call's last spins
-        if (waited < std::chrono::microseconds(100)) continue;
-        if (waited > kOneWaitLimit) {
-          if (by_resident) (void)stop_resident();  // bounded; marks the context wedged
-          if (!wedged) g_last_error = "latency kernel gave no answer within 10 s";
-          return NOISE_GPU_E_HIP;
-        }
-        const hipError_t e = hipStreamQuery(wst);
-        if (e == hipSuccess) {
-          if (*done == s) return NOISE_GPU_OK;
-          if (by_resident && launched) {  // the instance idled out before the doorbell
-            const int rc = launch_resident(s - 1u);
-            if (rc) return rc;
-            continue;
-          }
-          g_last_error = "latency kernel ended without its done word";
-          return NOISE_GPU_E_HIP;
-        }
-        if (e != hipErrorNotReady) return hip_fail(e, "latency kernel");
+      // now and then: has the stream failed or ended?  A record takes
+      // microseconds: the stream query (a runtime call of ~1 us) is for the
+      // rare stall, not for every call's last spins
+      if ((spin & 1023u) != 1023u || waited < std::chrono::microseconds(100)) continue;
+      const hipError_t e = hipStreamQuery(wst);
+      if (e == hipSuccess) {
+        if (*done == s) return NOISE_GPU_OK;
+        // idled out: its alive word is 0, relaunched above
+        if (by_resident && launched && *alive() == 0u) continue;
+        g_last_error = "latency kernel ended without its done word";
+        return NOISE_GPU_E_HIP;
       }
+      if (e != hipErrorNotReady) return hip_fail(e, "latency kernel");
     }
   }
 };
@@ -524,6 +549,9 @@ int one_record(bool dec, const uint8_t key[32], uint64_t nonce, const uint8_t *a
     const uint32_t nlo = (uint32_t)nonce, nhi = (uint32_t)(nonce >> 32);
     chk += noise_amd::req_check_mix(0u, meta, nlo, nhi) + noise_amd::req_check_mix(1u, k[0], k[1], k[2]) +
            noise_amd::req_check_mix(2u, k[3], k[4], k[5]) + noise_amd::req_check_mix(3u, k[6], k[7], 0u);
+#if defined(NOISE_HIP_EMU)
+    chk ^= noise_amd::emu_req_check_flip;  // tools/emu only: a request line the instance must refuse
+#endif
     __m128i *q = reinterpret_cast<__m128i *>(c.hreq);
     _mm_store_si128(q + 1, _mm_setr_epi32((int)s, (int)k[0], (int)k[1], (int)k[2]));
     _mm_store_si128(q + 2, _mm_setr_epi32((int)s, (int)k[3], (int)k[4], (int)k[5]));

@@ -87,6 +87,13 @@ __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// A/B knob (round 5): the Poly1305 pass's DMAs with the default policy
+#ifdef NOISE_POLY_DMA_PLAIN
+constexpr bool kPolyDmaPlain = true;
+#else
+constexpr bool kPolyDmaPlain = false;
+#endif
+
 // Record addressing / keying of a tile launch.
 enum TileMode : int {
   kTileUniform = 0,   // one key, nonce0 + i, record i at in + i*in_stride
@@ -191,6 +198,9 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
   using C = TileCfg<L, SPAN>;
   if (ABL == 1) return;
   constexpr bool TAGGED_IN = DECRYPT && MODE < kTileSeg;  // ct || tag pieces
+  // every record byte is read once (nt), except that the decrypt's Poly1305
+  // pass reads the ciphertext the keystream pass reads again
+  constexpr bool NT = !(MODE == kTileSegPoly && kPolyDmaPlain);
   constexpr int IN_SLOTS = TAGGED_IN ? C::NSLOT : C::REC_SLOTS;
   if (CONTIG) {
     // slot s = 64q + lane holds piece swz(s) = 64q + glq(gl, q); packed
@@ -205,7 +215,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
       for (int q = 0; q < C::REC_SLOTS / 64; ++q) {
         const uint32_t g = 64u * q + glq<SPAN>(gl, q);
         const uint32_t rr = g / C::SPR;
-        lds_dma16_s(base, DECRYPT ? 16u * (g + rr) : 16u * g, (lds_void *)(lds3 + 64 * q));
+        lds_dma16_s<NT>(base, DECRYPT ? 16u * (g + rr) : 16u * g, (lds_void *)(lds3 + 64 * q));
       }
     } else {
 #pragma unroll
@@ -213,7 +223,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
         const uint32_t g = 64u * q + glq<SPAN>(gl, q);
         const uint32_t rr = g / C::SPR;
         const uint32_t off = DECRYPT ? 16u * (g + rr) : 16u * g;
-        if (rr < nv) lds_dma16_s(base, off, (lds_void *)(lds3 + 64 * q));
+        if (rr < nv) lds_dma16_s<NT>(base, off, (lds_void *)(lds3 + 64 * q));
       }
     }
     if (TAGGED_IN) {  // tag pieces: slot REC_SLOTS + r <- piece (r, SPR)
@@ -221,7 +231,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
       for (int q = C::REC_SLOTS / 64; q < (C::NSLOT + 63) / 64; ++q) {
         const uint32_t r = 64u * q + lane - C::REC_SLOTS;
         if (r < nv)
-          lds_dma16_s(base, 16u * (r * (C::SPR + 1) + C::SPR), (lds_void *)(lds3 + 64 * q));
+          lds_dma16_s<NT>(base, 16u * (r * (C::SPR + 1) + C::SPR), (lds_void *)(lds3 + 64 * q));
       }
     }
   } else if (MODE >= kTileSeg || (MODE == kTileDesc && C::SPR == 64)) {
@@ -235,7 +245,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
         const uint32_t kl = t_rpt + q;
         const uint64_t off = join64((uint32_t)__builtin_amdgcn_readlane((int)own_in_hi, (int)kl),
                                     (uint32_t)__builtin_amdgcn_readlane((int)own_in_lo, (int)kl));
-        lds_dma16_s(in + off, 16u * glq<SPAN>(gl, q), (lds_void *)(lds3 + 64 * q));
+        lds_dma16_s<NT>(in + off, 16u * glq<SPAN>(gl, q), (lds_void *)(lds3 + 64 * q));
       }
     }
     if (TAGGED_IN) {  // decrypt: the RPT tags, lane r -> slot REC_SLOTS + r
@@ -243,7 +253,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
       const uint64_t off = ((uint64_t)(uint32_t)__shfl((int)own_in_hi, (int)(t_rpt + r)) << 32) |
                            (uint32_t)__shfl((int)own_in_lo, (int)(t_rpt + r));
       if (lane < (uint32_t)C::RPT && lane < nv)
-        lds_dma16_v(in + off + 16u * C::SPR, (lds_void *)(lds3 + C::REC_SLOTS));
+        lds_dma16_v<NT>(in + off + 16u * C::SPR, (lds_void *)(lds3 + C::REC_SLOTS));
     }
   } else {
 #pragma unroll 1
@@ -268,7 +278,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
         rec_base = in + (rec0 + r) * in_stride;
       }
       if (s < (uint32_t)IN_SLOTS && r < nv)
-        lds_dma16_v(rec_base + 16u * p, (lds_void *)(lds3 + 64 * q));
+        lds_dma16_v<NT>(rec_base + 16u * p, (lds_void *)(lds3 + 64 * q));
     }
   }
 }
@@ -367,6 +377,8 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
   static_assert(!SEG || (L == 1024 && (SPAN == 256 || SPAN == 128)),
                 "segments are 1 KiB, 256 or 128 B per lane");
   static_assert(NBUF == 1 || NBUF == 2, "one or two tile buffers");
+  // the Poly1305 pass issues the next tile's DMA into buffer 0 itself
+  static_assert(MODE != kTileSegPoly || NBUF == 1, "the Poly1305 pass has one tile buffer");
   __shared__ uint4 lds[NBUF * C::NSLOT];
   const uint32_t lane = threadIdx.x;
   const uint8_t *in = a.in;

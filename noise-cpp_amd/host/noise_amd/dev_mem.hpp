@@ -67,4 +67,21 @@ inline hipError_t dev_wipe_free(void *p, size_t bytes, hipStream_t stream) {
   return e != hipSuccess ? e : e2;
 }
 
+// dev_alloc / dev_wipe_free work on the CURRENT device (their pool choice
+// is per device): an owner bound to one device (a Pipeline) holds this guard
+// around them, so the allocation, its free and every HIP call in between
+// target the owner's device whatever device the calling thread has current
+struct DeviceGuard {
+  int prev = -1, want;
+  explicit DeviceGuard(int dev) : want(dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != want) (void)hipSetDevice(want);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0 && prev != want) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard &) = delete;
+  DeviceGuard &operator=(const DeviceGuard &) = delete;
+};
+
 }  // namespace noise_amd

@@ -357,18 +357,17 @@ Pipeline::~Pipeline() {
   // (dev_mem.hpp), after sync_all: no device-wide wait, so a resident latency
   // instance serving another thread does not hold this up.  (hipHostFree
   // below still waits for every stream of the device: noise_gpu.h.)
+  // Everything below on the Pipeline's device (the frees, their
+  // pool choice and the records scratch release all follow the current device)
+  const noise_amd::DeviceGuard on_dev(dev_);
   if (d_keys_) {
     (void)dev_wipe_free(d_keys_, 32 * key_cap_, slots_[0]->st);
     (void)hipStreamSynchronize(slots_[0]->st);
   }
   // the records scratch and companion stream cached for each slot stream go
-  // with it (on the Pipeline's device)
-  int cur = dev_;
-  (void)hipGetDevice(&cur);
-  if (cur != dev_) (void)hipSetDevice(dev_);
+  // with it
   for (Slot *sl : slots_)
     if (sl->st) (void)noise_gpu_scratch_release(sl->st);
-  if (cur != dev_) (void)hipSetDevice(cur);
   for (Slot *sl : slots_) {
     if (sl->d && sl->st) {  // the messages in and out: wiped, then freed
       (void)dev_wipe_free(sl->d, slot_total_, sl->st);
@@ -398,6 +397,7 @@ void Pipeline::grow_keys() {
   // (sync_all also waits until the launcher has issued every flushed slot, so
   // nothing else enqueues on slot 0's stream, which carries the table below)
   sync_all();
+  const noise_amd::DeviceGuard on_dev(dev_);  // the table lives on the Pipeline's device
   const std::size_t cap = key_cap_ ? 2 * key_cap_ : 1024;
   hipStream_t ks = slots_[0]->st;
   std::uint8_t *h = nullptr, *d = nullptr;
@@ -675,6 +675,9 @@ std::uint64_t Pipeline::flush() {
 }
 
 void Pipeline::enqueue(const LaunchJob &j) {
+  // flush() without the launcher thread runs this on the caller's thread:
+  // the records call's scratch and companion stream are per (device, stream)
+  const noise_amd::DeviceGuard on_dev(dev_);
   Slot &sl = *j.sl;
   const bool dec = dir_ == Direction::Decrypt;
   // Key rows reach the device table on the stream of the slot that first

@@ -295,3 +295,65 @@ def test_mixed_batch_zero_key_rows(oracle):
             assert back[o:o + L] == b"\x77" * L, ("nothing written", i, L)
         else:
             assert st[i] == noise_amd.REC_OK and back[o:o + L] == pts[i], (i, L)
+
+
+@pytest.mark.parametrize("in_place", [False, True])
+def test_chunked_decrypt_pipeline_tamper(oracle, in_place):
+    """Batches of >= 65536 records run the verify-first decrypt of the long
+    records in kSegChunks chunks over three streams (records_kernels.hip
+    launch_classes: Poly1305 pass + tag check on the caller's stream, the
+    segments' keystream pass on the second companion stream, the tails' on
+    the first, joined by the fin[c] / xdone / join2 events).  Tampered long
+    records (with and without tails; ct and tag bytes) sit in every chunk:
+    their status is BAD_MAC, a failed copy's output is zeroed, a failed
+    in-place record keeps its ciphertext, and every other record matches the
+    oracle -- on the GPU, where those events really order the passes
+    (crypto_aead_read, monocypher.c:2912-2929)."""
+    rng = random.Random(4242 + in_place)
+    nkeys = 11
+    keys = [rng.randbytes(32) for _ in range(nkeys)]
+    longs = [1024 * 2, 1024 * 5 + 1, 16384, 16385, 65519, 40001, 1024 * 9 + 1009, 3071, 32768, 20000]
+    recs = []
+    for i in range(70000):
+        if i % 70 == 35:
+            L = longs[(i // 70) % len(longs)]
+        else:
+            L = 64 if i % 3 else 128
+        recs.append([L, b"", rng.randrange(nkeys), rng.getrandbits(64) % (2**64 - 2), 0, 0])
+    pts = [rng.randbytes(r[0]) for r in recs]
+    long_idx = [i for i, r in enumerate(recs) if r[0] > 1024]
+    assert len(long_idx) == 1000
+    # every 13th long record is tampered: ~77, spread over the record order
+    # (the chunks split the long records in record order)
+    bad = set(long_idx[5::13])
+    cts = []
+    for i, (L, ad, ki, n, _, _) in enumerate(recs):
+        ct = bytearray(oracle.encrypt(keys[ki], n, ad, pts[i]))
+        if i in bad:
+            pos = rng.randrange(L + 16) if rng.random() < 0.7 else L + rng.randrange(16)
+            ct[pos] ^= 1 << rng.randrange(8)
+        cts.append(ct)
+    ddesc, din, dout, _ = layout(recs, decrypt=True, in_place=in_place)
+    cin = bytearray(din)
+    fill(cin, ddesc, cts, "in_off")
+    snapshot = bytes(cin)
+    d_keys, d_desc = dev(b"".join(keys)), dev(ddesc.view(np.uint8))
+    d_in = dev(cin)
+    d_out = d_in if in_place else torch.full((dout,), 0x3C, dtype=torch.uint8, device="cuda")
+    d_st = torch.full((len(recs),), 9, dtype=torch.uint8, device="cuda")
+    noise_amd.decrypt_records(d_keys, nkeys, d_desc, len(recs), d_in, d_out, d_st, None)
+    st = host(d_st)
+    back = host(d_out)
+    for i, (L, *_rest) in enumerate(recs):
+        o = int(ddesc[i]["out_off"])
+        if i in bad:
+            assert st[i] == noise_amd.REC_BAD_MAC, (i, L)
+            if in_place:
+                assert back[o:o + L + 16] == snapshot[o:o + L + 16], ("in-place failure must keep ct", i, L)
+            else:
+                assert back[o:o + L] == bytes(L), ("failed copy must be zeroed", i, L)
+        else:
+            assert st[i] == noise_amd.REC_OK, (i, L, st[i])
+            assert back[o:o + L] == pts[i], (i, L)
+        if not in_place:
+            assert back[o + L:o + L + 16] == b"\x3c" * 16, ("wrote past the record", i, L)

@@ -10,10 +10,19 @@
 // of the latency path's mapped staging.
 //
 //   emu_api            -> "emu_api ok (N calls, M scans)" or FAIL lines
+#include <dirent.h>
+#include <sanitizer/common_interface_defs.h>
+#include <signal.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <thread>
 #include <vector>
 
 #include <hip/hip_runtime.h>
@@ -23,6 +32,7 @@
 
 namespace noise_amd {  // single_kernels.hip: emulated asynchronously (below)
 void k_aead_resident(uint8_t *req, uint8_t *base, uint32_t last, uint64_t idle_ticks);
+extern uint32_t emu_req_check_flip;  // noise_gpu_api.hip (emulation build only)
 }
 
 extern "C" {
@@ -33,7 +43,52 @@ int oracle_noise_decrypt(const uint8_t key[32], uint64_t n, const uint8_t *ad, s
 void oracle_rekey(const uint8_t key[32], uint8_t out[32]);
 }
 
-static int fails = 0, scans = 0, calls = 0;
+static int fails = 0, scans = 0;
+static std::atomic<int> calls{0};
+static std::atomic<const char *> phase{"start"};
+
+// Watchdog: a progress line on stderr every 30 s (calls done, phase); after
+// 120 s without a finished call it prints every thread's stack (SIGUSR2 to
+// each task of the process; the handler prints its own thread's stack with
+// the sanitizer's unwinder), once, so a stall names itself instead of
+// running into the test's time limit.
+static void stack_handler(int) { __sanitizer_print_stack_trace(); }
+static void dump_all_stacks() {
+  signal(SIGUSR2, stack_handler);
+  const pid_t me = (pid_t)syscall(SYS_gettid);
+  if (DIR *d = opendir("/proc/self/task")) {
+    while (dirent *e = readdir(d)) {
+      const pid_t tid = (pid_t)std::atoi(e->d_name);
+      if (tid <= 0 || tid == me) continue;
+      std::fprintf(stderr, "---- thread %d\n", (int)tid);
+      syscall(SYS_tgkill, getpid(), tid, SIGUSR2);
+      std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    }
+    closedir(d);
+  }
+}
+static void start_watchdog() {
+  std::thread([] {
+    using namespace std::chrono;
+    const auto t0 = steady_clock::now();
+    auto last_change = t0;
+    int last_calls = -1;
+    bool dumped = false;
+    for (;;) {
+      std::this_thread::sleep_for(seconds(30));
+      const auto now = steady_clock::now();
+      const int c = calls.load();
+      if (c != last_calls) last_calls = c, last_change = now;
+      std::fprintf(stderr, "[emu_api watchdog] %.0f s: %d calls, phase %s\n",
+                   duration<double>(now - t0).count(), c, phase.load());
+      if (!dumped && now - last_change > seconds(120)) {
+        dumped = true;
+        std::fprintf(stderr, "[emu_api watchdog] no call finished for 120 s: stacks of every thread\n");
+        dump_all_stacks();
+      }
+    }
+  }).detach();
+}
 #define CHECK(c, ...)                      \
   do {                                     \
     if (!(c)) {                            \
@@ -63,7 +118,39 @@ static void scan(const char *after, bool resident = false) {
   }
 }
 
+// each phase's start on stdout with the time since the run began
+static const auto g_t0 = std::chrono::steady_clock::now();
+static void enter(const char *what) {
+  phase = what;
+  std::printf("[%7.1f s] %s\n",
+              std::chrono::duration<double>(std::chrono::steady_clock::now() - g_t0).count(), what);
+  std::fflush(stdout);
+}
+
+static void refused_request(const char *what, double limit_s, const uint8_t key[32], std::mt19937_64 &rng) {
+  enter(what);
+  std::vector<uint8_t> buf(64 + 16), pt(64), want(64 + 16);
+  for (auto &x : pt) x = (uint8_t)rng();
+  std::memcpy(buf.data(), pt.data(), 64);
+  noise_amd::emu_req_check_flip = 0x00010000u;
+  const auto t0 = std::chrono::steady_clock::now();
+  ++calls;
+  int rc = noise_gpu_encrypt_host(key, 5, nullptr, 0, buf.data(), 64);
+  const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  noise_amd::emu_req_check_flip = 0u;
+  CHECK(rc == NOISE_GPU_E_HIP && secs < limit_s, "refused request (%s): rc=%d after %.1f s", what, rc, secs);
+  std::printf("refused request (%s): rc %d after %.2f s (%s)\n", what, rc, secs, noise_gpu_last_error());
+  scan("refused request", true);
+  oracle_noise_encrypt(key, 6, nullptr, 0, pt.data(), 64, want.data());
+  std::memcpy(buf.data(), pt.data(), 64);
+  ++calls;
+  rc = noise_gpu_encrypt_host(key, 6, nullptr, 0, buf.data(), 64);
+  CHECK(rc == NOISE_GPU_OK && buf == want, "after the refused request (%s): rc=%d", what, rc);
+  scan("after the refused request", true);
+}
+
 int main() {
+  start_watchdog();
   std::mt19937_64 rng(12345);
   auto rbytes = [&](size_t n) {
     std::vector<uint8_t> v(n);
@@ -73,6 +160,7 @@ int main() {
   uint8_t key[32];
   for (auto &x : key) x = (uint8_t)rng();
   // ---- single records: latency kernel (AD <= 8192) and the staged path
+  enter("single records (launch mode)");
   const size_t lens[] = {0, 1, 15, 16, 17, 63, 64, 65, 100, 1000, 1024, 1040, 4096, 5000, 16384,
                          65519, 65535, 70000};
   const size_t ads[] = {0, 7, 64, 100, 9000};
@@ -105,6 +193,7 @@ int main() {
   // ---- single records through the resident latency kernel (opt-in): the
   // emulated launch runs it to its idle exit, so every further request is
   // picked up by a relaunch from the host's wait loop (the lost-doorbell path)
+  enter("resident, synchronous instances");
   CHECK(noise_gpu_set_resident(1, 300) == NOISE_GPU_OK, "set_resident on");
   CHECK(noise_gpu_set_resident(1, 20000000) == NOISE_GPU_E_ARG, "idle above 10 s refused");
   for (size_t L : {0ul, 17ul, 1024ul, 4096ul, 65535ul, 70000ul})
@@ -137,6 +226,12 @@ int main() {
   // limits (63 keystream blocks, 256 Poly1305 blocks), tampering included.
   // The resident kernel runs asynchronously here (as on a GPU: one instance
   // serves many requests) with a long idle time, so its slots survive.
+  // a request line no instance takes (its check word corrupted): every
+  // relaunched instance sees it whole on its first poll and refuses it, so
+  // the host's wait gives up after its relaunch cap -- E_HIP at once, not a
+  // loop -- and the next call on the context works
+  refused_request("synchronous instances", 15.0, key, rng);
+  enter("resident, one asynchronous instance");
   emu::async_kernel = reinterpret_cast<void *>(&noise_amd::k_aead_resident);
   CHECK(noise_gpu_set_resident(1, 5000000) == NOISE_GPU_OK, "set_resident long idle");
   {
@@ -188,7 +283,12 @@ int main() {
         }
       }
   }
+  // the same with one long-lived instance that keeps polling: the host's
+  // wait runs into its 10-s limit, stops the instance (bounded) and fails
+  // the call; the next call relaunches and works
+  refused_request("asynchronous instance", 15.0, key, rng);
   CHECK(noise_gpu_set_resident(0, 0) == NOISE_GPU_OK, "set_resident off");
+  enter("rekey, batches, contexts");
   emu::async_kernel = nullptr;
   // ---- rekey
   for (int i = 0; i < 4; ++i) {
@@ -337,9 +437,9 @@ int main() {
   CHECK(noise_gpu_thread_release() == NOISE_GPU_OK, "thread_release");
   CHECK(emu::allocations().empty(), "thread_release left %zu allocations", emu::allocations().size());
   if (fails) {
-    std::printf("emu_api FAIL (%d failures, %d calls, %d scans)\n", fails, calls, scans);
+    std::printf("emu_api FAIL (%d failures, %d calls, %d scans)\n", fails, calls.load(), scans);
     return 1;
   }
-  std::printf("emu_api ok (%d calls, %d scans)\n", calls, scans);
+  std::printf("emu_api ok (%d calls, %d scans)\n", calls.load(), scans);
   return 0;
 }

@@ -94,6 +94,19 @@ def reduce_over_ranks(dist, elapsed, nrec, device):
     return float(t.item()), int(n.item())
 
 
+def device_info(args, local):
+    """The rank's device: index, name and PCI bus id (the stub: the host)."""
+    if args.stub:
+        return {"index": None, "name": "cpu (stub)"}
+    import torch
+    p = torch.cuda.get_device_properties(local)
+    info = {"index": local, "name": p.name}
+    for k in ("pci_domain_id", "pci_bus_id", "pci_device_id"):
+        if hasattr(p, k):
+            info[k] = getattr(p, k)
+    return info
+
+
 def check_shards(shards):
     """Rank shard table -> error text if two ranks share a nonce."""
     spans = sorted((s["nonce_lo"], s["nonce_hi"], s["rank"]) for s in shards)
@@ -399,8 +412,14 @@ def tile_symbol(dec, L, contig, mode):
 def make_stub_workload(args, rank, world):
     """--stub: host-only stand-in with the real shard bookkeeping."""
     import numpy as np
-    R, L = args.records or 1024, 64
-    n_base = rank_nonce_base(2, rank, world, R, R * world)
+    if args.config == 5:  # strong scaling: this rank's slice of one 8 Mi-record range
+        total = args.records or (8 << 20)
+        lo, hi = shard(total, rank, world)
+        R, L = hi - lo, 16
+        n_base = rank_nonce_base(5, rank, world, R, total)
+    else:
+        R, L = args.records or 1024, 64
+        n_base = rank_nonce_base(2, rank, world, R, R * world)
     buf = np.zeros(R * L, dtype=np.uint8)
 
     def step(evs=None):
@@ -731,7 +750,16 @@ def main(argv=None):
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    mine = {"rank": rank, "nonce_lo": wl["n_base"], "nonce_hi": wl["n_base"] + R, "records": R}
+    if evs:
+        enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+        dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+    else:
+        enc_ms = dec_ms = elapsed * 1e3 / args.steps / 2
+    # this rank's own figures: with them the N-GPU line shows each GPU's
+    # balance beside the max-over-ranks wall time
+    mine = {"rank": rank, "nonce_lo": wl["n_base"], "nonce_hi": wl["n_base"] + R, "records": R,
+            "enc_ms": round(enc_ms, 4), "dec_ms": round(dec_ms, 4),
+            "step_ms": round(elapsed * 1e3 / args.steps, 4), "device": device_info(args, local)}
     # the timed work was correct too
     if not wl["check"]():
         raise SystemExit("timed round trip failed on rank %d" % rank)
@@ -756,11 +784,6 @@ def main(argv=None):
     bad = check_shards(shards) if cfg != 3 else None
     if bad:
         raise SystemExit("shard table: " + bad)
-    if evs:
-        enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
-        dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
-    else:
-        enc_ms = dec_ms = elapsed * 1e3 / args.steps / 2
     log("enc %.3f ms, dec %.3f ms per launch; step %.3f ms" %
         (enc_ms, dec_ms, elapsed * 1e3 / args.steps))
 

@@ -873,11 +873,19 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_resident(uint8_t *req, uint8
         // issue slots; a request that follows the previous one within a few
         // ms is still seen at the full poll rate
         if (polls >= NOISE_RES_SLEEP_POLLS) __builtin_amdgcn_s_sleep(32);
-        if ((++polls & 31u) == 0u &&
-            (__hip_atomic_load(&ring->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
-             __builtin_amdgcn_s_memrealtime() - t_last > idle_ticks)) {
-          ex = 1;
-          break;
+        if ((++polls & 31u) == 0u) {
+          // ONE decision for the wave (lane 0's).  On the GPU the stop word
+          // is one load instruction and the clock a scalar read, so the lanes
+          // agree anyway; the CPU emulator runs lanes as threads, which read
+          // them at different times: a lane that saw the stop word (or the
+          // idle deadline) flip first left the loop alone, the others waited
+          // in the next __shfl for it for ever (emu_api's round-4 hang)
+          const bool leave = __hip_atomic_load(&ring->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+                             __builtin_amdgcn_s_memrealtime() - t_last > idle_ticks;
+          if (__builtin_amdgcn_readfirstlane((int)leave)) {
+            ex = 1;
+            break;
+          }
         }
       }
       if (!ex) {

@@ -120,7 +120,7 @@ enum TileMode : int {
 // (Horner in R = r^64), appends the tail (k_seg_tail: the len % 1024 bytes
 // past the last full segment, one lane per tail) as h r^(tail blocks) +
 // P_tail, then the length block and the tag.
-struct SegRec {                  // one per long record, 256 B (two 128-B lines)
+struct SegRec {                  // one per long record, 384 B (three 128-B lines)
   uint64_t in_off, out_off, nonce, seg0;  // seg0: index of segment 0
   uint32_t k[8];                 // the record's key (copied from the key table)
   uint32_t key_idx, di, len, nfull;       // di: descriptor index
@@ -132,8 +132,11 @@ struct SegRec {                  // one per long record, 256 B (two 128-B lines)
   uint32_t ok;                   // decrypt: 1 once the finalize kernel verified the tag
   uint32_t pw8[5];               // r^8 (radix 2^26): the 128-B span passes
   uint32_t pad[5];
+  // decrypt (unit_kernel.hpp): R^2, R^4, R^8, R^16, R^32 for R = r^64 (radix 2^26)
+  uint32_t rpow[5][5];
+  uint32_t pad2[7];
 };
-static_assert(sizeof(SegRec) == 256, "SegRec layout");
+static_assert(sizeof(SegRec) == 384, "SegRec layout");
 struct SegEntry {                // one per full segment
   uint32_t q, s;                 // long-record index, segment number
 };

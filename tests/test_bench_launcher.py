@@ -43,6 +43,39 @@ def test_launcher_spawns_ranks_one_json_line(gpus):
     assert d["value"] > 0 and d["config"]["records_per_gpu"] == 100
 
 
+def test_launcher_eight_ranks_per_rank_fields():
+    """The driver's 8-GPU shape, rehearsed on the CPU: 8 ranks over gloo, one
+    JSON line with n_gpus = 8, and each shard entry carries the rank's own
+    encrypt / decrypt / step times and device, so the 8-GPU line shows every
+    GPU's balance beside the max-over-ranks wall rate."""
+    p = run_bench("--records", "256", gpus=8, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8
+    shards = sorted(d["shards"], key=lambda s: s["rank"])
+    assert [s["rank"] for s in shards] == list(range(8))
+    for s in shards:
+        assert s["enc_ms"] > 0 and s["dec_ms"] > 0 and s["step_ms"] > 0
+        assert "device" in s and "name" in s["device"]
+    # the line's wall time is the max over ranks
+    assert d["ms_per_step"] >= max(s["step_ms"] for s in shards) * 0.999
+
+
+def test_launcher_config5_eight_ranks_one_nonce_range():
+    """Config 5 (strong scaling) at N = 8: one 8 Mi-record nonce range split
+    contiguously, rank r holds 1 Mi records at nonce base r * 2^20 (SURVEY
+    8(e); bench.py shard / rank_nonce_base, the same code the GPU run uses)."""
+    p = run_bench("--config", "5", gpus=8, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["n_gpus"] == 8 and d["scaling"] == "strong"
+    shards = sorted(d["shards"], key=lambda s: s["rank"])
+    assert [(s["nonce_lo"], s["nonce_hi"], s["records"]) for s in shards] == \
+        [(r << 20, (r + 1) << 20, 1 << 20) for r in range(8)]
+
+
 def test_single_gpu_path_does_not_launch():
     p = run_bench("--records", "64", gpus=1)
     assert p.returncode == 0, p.stderr[-2000:]

@@ -188,8 +188,17 @@ int main(int argc, char **argv) {
           }
     } else {
       CHECK(st[i] == 0, "status of record %llu len %u = %u", (unsigned long long)i, L, st[i]);
-      CHECK(std::memcmp(back + dec[i].out_off, pt_copy.data() + (enc[i].in_off - gap), L) == 0,
-            "decrypt record %llu len %u", (unsigned long long)i, L);
+      {
+        uint32_t bad = 0, first = L, nbad = 0;
+        for (uint32_t b = 0; b < L; ++b)
+          if (back[dec[i].out_off + b] != pt_copy[enc[i].in_off - gap + b]) {
+            if (first == L) first = b;
+            ++nbad;
+          }
+        bad = nbad;
+        CHECK(bad == 0, "decrypt record %llu len %u (%u bytes differ, first at %u)", (unsigned long long)i, L,
+              nbad, first);
+      }
     }
   }
   std::printf("%s R=%llu bytes=%llu: %s (%d failures)\n", mode, (unsigned long long)R,

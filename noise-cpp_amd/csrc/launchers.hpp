@@ -87,16 +87,22 @@ __host__ __device__ constexpr bool req_inline(uint32_t ad_len, uint32_t len, boo
 __host__ __device__ constexpr uint32_t req_inline_chunks(uint32_t ad_len, uint32_t len, bool decrypt) {
   return req_inline(ad_len, len, decrypt) ? (req_image_bytes(ad_len, len, decrypt) + 11u) / 12u : 0u;
 }
-// The request's check word (chunk 3, word 3): a position-weighted 32-bit sum
-// of the three payload words of every header chunk (chunk 3 counts with its
-// check word as 0) and every inline chunk.  The kernel takes a request only
-// when all its chunks carry the new seq AND their words sum to the check
-// word, so a chunk whose 16-byte BAR store has landed in part (new seq,
-// stale payload) is polled again instead of served.
-constexpr uint32_t kReqCheckSalt = 0x9e3779b9u;
-__host__ __device__ constexpr uint32_t req_check_mix(uint32_t chunk, uint32_t w1, uint32_t w2,
+// Every chunk of a request carries its own check: its first word is
+// seq ^ req_chunk_tag(chunk, w1, w2, w3) over its three payload words.  The
+// kernel decodes each chunk it polls and takes a request only when the four
+// header chunks (and every inline chunk) decode to the same new seq, so a
+// chunk whose 16-byte BAR store landed in part (new first word, stale
+// payload, or the reverse) decodes to something else and is polled again.
+// The check is per lane, folded into the seq compare (round 5): round 4's
+// single check word needed a cross-lane sum on the accept path.  The chunk
+// constant keeps an all-zero image (never a request) from decoding to one
+// seq in all four header chunks.
+__host__ __device__ constexpr uint32_t req_rotl(uint32_t x, int n) {
+  return (x << n) | (x >> (32 - n));
+}
+__host__ __device__ constexpr uint32_t req_chunk_tag(uint32_t chunk, uint32_t w1, uint32_t w2,
                                                      uint32_t w3) {
-  return w1 * (6u * chunk + 1u) + w2 * (6u * chunk + 3u) + w3 * (6u * chunk + 5u);
+  return req_rotl(w1, 7) ^ req_rotl(w2, 19) ^ w3 ^ (0x9e3779b9u * (chunk + 1u));
 }
 __host__ __device__ constexpr OneLayout one_layout(uint32_t ad_len, uint32_t len) {
   const uint64_t a16 = (ad_len + 15ull) & ~15ull, l16 = (len + 15ull) & ~15ull;

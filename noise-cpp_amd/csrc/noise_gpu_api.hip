@@ -380,9 +380,6 @@ struct OneCtx {
     if (rstream) return NOISE_GPU_OK;
     int least = 0, greatest = 0;
     HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-#ifdef NOISE_RES_NORMAL_PRIO  // A/B only: a normal-priority stream (shares a queue with the others)
-    greatest = least;
-#endif
     HIP_TRY(hipStreamCreateWithPriority(&rstream, hipStreamNonBlocking, greatest));
     return NOISE_GPU_OK;
   }
@@ -510,7 +507,6 @@ int one_record(bool dec, const uint8_t key[32], uint64_t nonce, const uint8_t *a
   uint32_t s = ++c.seq;
   if (s == 0) s = c.seq = 1;
   const uint32_t n_inl = res ? noise_amd::req_inline_chunks(ad_len, len, dec) : 0u;
-  uint32_t chk = noise_amd::kReqCheckSalt;  // the request's check word (launchers.hpp)
   if (n_inl) {
     // a small record goes inline: its staged image (AD | pad | record | pad
     // | tag) 12 bytes per 16-byte chunk {seq, 3 words} (launchers.hpp OneReq)
@@ -524,8 +520,8 @@ int one_record(bool dec, const uint8_t key[32], uint64_t nonce, const uint8_t *a
     for (uint32_t i = 0; i < n_inl; ++i) {
       uint32_t w[3];
       std::memcpy(w, im + 12u * i, 12);
-      chk += noise_amd::req_check_mix(4u + i, w[0], w[1], w[2]);
-      _mm_store_si128(q + i, _mm_setr_epi32((int)s, (int)w[0], (int)w[1], (int)w[2]));
+      const uint32_t x = s ^ noise_amd::req_chunk_tag(4u + i, w[0], w[1], w[2]);
+      _mm_store_si128(q + i, _mm_setr_epi32((int)x, (int)w[0], (int)w[1], (int)w[2]));
       w[0] = w[1] = w[2] = 0u;
     }
     explicit_bzero(im, 12u * n_inl);  // the plaintext copy on the stack goes too
@@ -540,25 +536,27 @@ int one_record(bool dec, const uint8_t key[32], uint64_t nonce, const uint8_t *a
   uint32_t k[8];
   key_words(key, k);
   if (res) {
-    // the request line: four 16-byte chunks, each {seq, 3 payload words},
-    // stored whole (16-byte aligned SSE stores) after an sfence that orders
-    // them behind the staged bytes (write-combined device memory); the GPU
-    // takes the request once all four (and any inline chunks) carry seq
+    // the request line: four 16-byte chunks, each {seq ^ its tag, 3 payload
+    // words} (launchers.hpp req_chunk_tag), stored whole (16-byte aligned SSE
+    // stores) after an sfence that orders them behind the staged bytes
+    // (write-combined device memory); the GPU takes the request once all four
+    // (and any inline chunks) decode to the new seq
     _mm_sfence();
     const uint32_t meta = len | (ad_len << 16) | ((uint32_t)dec << 30);
     const uint32_t nlo = (uint32_t)nonce, nhi = (uint32_t)(nonce >> 32);
-    chk += noise_amd::req_check_mix(0u, meta, nlo, nhi) + noise_amd::req_check_mix(1u, k[0], k[1], k[2]) +
-           noise_amd::req_check_mix(2u, k[3], k[4], k[5]) + noise_amd::req_check_mix(3u, k[6], k[7], 0u);
+    uint32_t x3 = s ^ noise_amd::req_chunk_tag(3u, k[6], k[7], 0u);
 #if defined(NOISE_HIP_EMU)
-    chk ^= noise_amd::emu_req_check_flip;  // tools/emu only: a request line the instance must refuse
+    x3 ^= noise_amd::emu_req_check_flip;  // tools/emu only: a request line the instance must refuse
 #endif
     __m128i *q = reinterpret_cast<__m128i *>(c.hreq);
-    _mm_store_si128(q + 1, _mm_setr_epi32((int)s, (int)k[0], (int)k[1], (int)k[2]));
-    _mm_store_si128(q + 2, _mm_setr_epi32((int)s, (int)k[3], (int)k[4], (int)k[5]));
-    _mm_store_si128(q + 3, _mm_setr_epi32((int)s, (int)k[6], (int)k[7], (int)chk));
-    _mm_store_si128(q + 0, _mm_setr_epi32((int)s, (int)meta, (int)nlo, (int)nhi));
+    _mm_store_si128(q + 1, _mm_setr_epi32((int)(s ^ noise_amd::req_chunk_tag(1u, k[0], k[1], k[2])), (int)k[0],
+                                          (int)k[1], (int)k[2]));
+    _mm_store_si128(q + 2, _mm_setr_epi32((int)(s ^ noise_amd::req_chunk_tag(2u, k[3], k[4], k[5])), (int)k[3],
+                                          (int)k[4], (int)k[5]));
+    _mm_store_si128(q + 3, _mm_setr_epi32((int)x3, (int)k[6], (int)k[7], 0));
+    _mm_store_si128(q + 0, _mm_setr_epi32((int)(s ^ noise_amd::req_chunk_tag(0u, meta, nlo, nhi)), (int)meta,
+                                          (int)nlo, (int)nhi));
     _mm_sfence();
-    chk = 0u;
     // (re)launch when no instance runs: never launched, or the last one left
     // on its idle timer (it clears the alive word on its way out, after its
     // last poll -- a request rung after that poll is this one's to serve)

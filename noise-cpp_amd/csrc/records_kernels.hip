@@ -29,8 +29,6 @@
 // Small batches (< kClassifyMin records) skip all this and run the generic
 // kernel directly (latency of single records from CipherState).
 // Scratch is a grow-only device buffer cached per (device, stream).
-#include <cstdlib>
-#include <cstring>
 #include <mutex>
 #include <vector>
 
@@ -38,7 +36,6 @@
 #include "launchers.hpp"
 #include "noise_amd/dev_mem.hpp"
 #include "tile_kernel.hpp"
-#include "unit_kernel.hpp"
 
 namespace noise_amd {
 
@@ -50,7 +47,7 @@ constexpr int kNumCls = kNumTileCls + 2;
 constexpr int kColSegs = kNumCls;         // classifier column: full segments
 constexpr int kColTails = kNumCls + 1;    // classifier column: long records with a tail
 constexpr int kColFin0 = kNumCls + 2;     // classifier columns: long records by
-constexpr int kFinBuckets = kUnitBuckets; // unit bucket (unit_kernel.hpp), 0..5
+constexpr int kFinBuckets = 6;            // floor(log2(full segments)), 1..63 -> 0..5
 constexpr int kCols = kNumCls + 2 + kFinBuckets;
 // Decrypt pipelines the long records in kSegChunks chunks (launch_classes):
 // the Poly1305 pass of chunk c + 1 (HBM-bound) runs beside the keystream pass
@@ -99,22 +96,6 @@ constexpr uint64_t kSegCapMax = NOISE_SEG_CAP;  // 16 Mi segments = 16 GiB per c
 #define NOISE_GRID_CAP 8192u
 #endif
 
-// Grid caps of the decrypt passes (A/B knobs; round 4: capping the keystream
-// pass at 3072 waves cost 12 %, the Poly1305 pass at 2048 nothing --
-// profiles/round4/ab/cfg4_verify_first.md section 6)
-#ifndef NOISE_POLY_GRID
-#define NOISE_POLY_GRID NOISE_GRID_CAP
-#endif
-#ifndef NOISE_XOR_GRID
-#define NOISE_XOR_GRID NOISE_GRID_CAP
-#endif
-
-// Grid cap of the unit kernel (4-wave workgroups looping over the units;
-// 2 resident per CU by LDS)
-#ifndef NOISE_UNIT_GRID
-#define NOISE_UNIT_GRID NOISE_GRID_CAP
-#endif
-
 // an all-zero key row is "no key" (Noise HasKey() false, e.g. the rows
 // noise_gpu_hs_split leaves for failed handshakes): never used to encrypt
 __device__ __forceinline__ bool key_row_zero(const uint8_t *keys, uint32_t ki) {
@@ -161,10 +142,10 @@ struct RecHdr {
 };
 static_assert(sizeof(RecHdr) == 8 * kHdrWords, "scratch header layout");
 
-// finalize-order bucket of a long record of `len` bytes (unit_kernel.hpp):
-// by its items m = nfull + (tail != 0), floor(log2(m - 1))
-__device__ __forceinline__ int fin_bucket(uint32_t len) {
-  return unit_bucket((len >> 10) + ((len & 1023u) != 0u ? 1u : 0u));
+// finalize-order bucket of a long record with nf >= 1 full segments
+__device__ __forceinline__ int fin_bucket(uint32_t nf) {
+  const int b = 31 - __builtin_clz(nf | 1u);
+  return b < kFinBuckets - 1 ? b : kFinBuckets - 1;
 }
 
 // wave-wide inclusive prefix sum (all 64 lanes participate)
@@ -211,11 +192,10 @@ __global__ __launch_bounds__(64) void k_cls_count(
   for (uint64_t i0 = b0; i0 < e0; i0 += 64) {
     const uint64_t i = i0 + lane;
     int cls = -1;
-    uint32_t nf = 0, d_len = 0;
+    uint32_t nf = 0;
     bool tail = false;
     if (i < e0) {
       const noise_gpu_record d = recs[i];
-      d_len = d.len;
       cls = record_class(d, keys, nkeys, in, out);
       nf = cls == kClsLong ? d.len >> 10 : 0u;
       tail = cls == kClsLong && (d.len & 1023u) != 0;
@@ -224,7 +204,7 @@ __global__ __launch_bounds__(64) void k_cls_count(
     for (int c = 0; c < kNumCls; ++c) cnt[c] += (uint32_t)__builtin_popcountll(__ballot(cls == c));
     nseg += wave_sum(nf);
     ntail += (uint32_t)__builtin_popcountll(__ballot(tail));
-    const int fb = cls == kClsLong ? fin_bucket(d_len) : -1;
+    const int fb = cls == kClsLong ? fin_bucket(nf) : -1;
 #pragma unroll
     for (int b = 0; b < kFinBuckets; ++b) fin[b] += (uint32_t)__builtin_popcountll(__ballot(fb == b));
   }
@@ -287,7 +267,7 @@ __global__ __launch_bounds__(64) void k_cls_scatter(
     const noise_gpu_record *__restrict__ recs, uint64_t nrec, uint32_t chunk,
     const uint8_t *keys, uint32_t nkeys, const uint8_t *in, const uint8_t *out,
     const unsigned long long *wbase, RecHdr *hdr, uint32_t *idx, SegRec *rt,
-    SegEntry *segs, uint32_t *tails, uint32_t *fin, uint32_t *finl, uint64_t segcap) {
+    SegEntry *segs, uint32_t *tails, uint32_t *fin, uint64_t segcap) {
   const uint32_t lane = threadIdx.x;
   const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
   const uint64_t e0 = b0 + chunk < nrec ? b0 + chunk : nrec;
@@ -344,17 +324,14 @@ __global__ __launch_bounds__(64) void k_cls_scatter(
       run[c] += (unsigned long long)__builtin_popcountll(m);
     }
     {  // long records in finalize order: by segment-count bucket
-      const int fb = cls == kClsLong ? fin_bucket(d.len) : -1;
+      const int fb = cls == kClsLong ? fin_bucket(nf) : -1;
 #pragma unroll
       for (int b = 0; b < kFinBuckets; ++b) {
         const uint64_t m = __ballot(fb == b);
-        if (fb == b) {
-          const unsigned long long pos =
-              fbase[b] + run[kColFin0 + b] +
-              __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-          fin[pos] = (uint32_t)q;
-          finl[pos] = d.len;  // the unit kernel's first load: record and length together
-        }
+        if (fb == b)
+          fin[fbase[b] + run[kColFin0 + b] +
+              __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+              (uint32_t)q;
         run[kColFin0 + b] += (unsigned long long)__builtin_popcountll(m);
       }
     }
@@ -427,7 +404,6 @@ __global__ __launch_bounds__(64) void k_cls_scatter(
 // k_seg_prep: lane per long record -> ChaCha block 0 (one-time key r, s),
 // r^16, r^32 (the segment kernel's 4-lane recombination) and r^64 (the
 // finalize kernel's Horner step over segments).
-template <bool RPOW>
 __global__ __launch_bounds__(64) void k_seg_prep(const uint8_t *__restrict__ keys,
                                                  SegRec *rt, const RecHdr *hdr) {
   const uint64_t n = hdr->nlong;
@@ -470,15 +446,6 @@ __global__ __launch_bounds__(64) void k_seg_prep(const uint8_t *__restrict__ key
       R.pw32[i] = x32.a[i];
       R.r64[i] = x64.a[i];
       R.rtail[i] = rt_pow.a[i];
-    }
-    if (RPOW) {  // the unit kernel's record weights R^(2^b), R = r^64
-      F26 y = x64;
-#pragma unroll
-      for (int b = 0; b < 5; ++b) {
-        y = mul26(y, y);
-#pragma unroll
-        for (int i = 0; i < 5; ++i) R.rpow[b][i] = y.a[i];
-      }
     }
   }
 }
@@ -966,39 +933,28 @@ template <bool DECRYPT>
 static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr *hdr,
                                  const uint8_t *keys, uint32_t nkeys,
                                  const noise_gpu_record *recs, const uint32_t *idx,
-                                 const uint32_t *tails, const uint32_t *fin, const uint32_t *finl,
-                                 uint64_t segbound,
+                                 const uint32_t *tails, const uint32_t *fin, uint64_t segbound,
                                  const uint8_t *in,
                                  uint8_t *out, const uint8_t *ad, uint8_t *status,
                                  hipStream_t stream, int chunks) {
   AuxStream ax;
   hipError_t e = aux_get(&ax, stream);
   if (e != hipSuccess) return e;
-#ifdef NOISE_RECORDS_SERIAL  // diagnostics only: every kernel on the caller's stream
-  ax.aux = stream;
-  ax.aux2 = stream;
-#endif
   const dim3 bt(64);
   const dim3 grid(capped((nrec + 63) / 64, NOISE_GRID_CAP));
   SegRec *rt = const_cast<SegRec *>(ta.rt);
-  // A/B (round 5): NOISE_GPU_LONG=segments selects the round-4 segment path
-  static const bool use_units = [] {
-    const char *e = std::getenv("NOISE_GPU_LONG");
-    return !(e && std::strcmp(e, "segments") == 0);
-  }();
   // fork right after the classifier: the small classes and the generic
   // kernel need nothing else; the tails also need k_seg_prep (prep event)
   if ((e = hipEventRecord(ax.fork, stream)) != hipSuccess) return e;
   if ((e = hipStreamWaitEvent(ax.aux, ax.fork, 0)) != hipSuccess) return e;
-  if (DECRYPT && use_units) hipLaunchKernelGGL((k_seg_prep<true>), grid, bt, 0, stream, keys, rt, hdr);
-  else hipLaunchKernelGGL((k_seg_prep<false>), grid, bt, 0, stream, keys, rt, hdr);
+  hipLaunchKernelGGL(k_seg_prep, grid, bt, 0, stream, keys, rt, hdr);
   if ((e = hipEventRecord(ax.prep, stream)) != hipSuccess) return e;
   TileArgs a = ta;
   const uint64_t gblocks = (nrec + kGenBlock - 1) / kGenBlock;
   const dim3 gg((unsigned)(gblocks < 2 * NOISE_GRID_CAP ? gblocks : 2 * NOISE_GRID_CAP));
   const dim3 gseg(capped((segbound + 63) / 64, NOISE_GRID_CAP));
-  const dim3 gpoly(capped((segbound + 63) / 64, NOISE_POLY_GRID));
-  const dim3 gxor(capped((segbound + 63) / 64, NOISE_XOR_GRID));
+  const dim3 gpoly(capped((segbound + 63) / 64, NOISE_GRID_CAP));
+  const dim3 gxor(capped((segbound + 63) / 64, NOISE_GRID_CAP));
   const dim3 gfin(capped((nrec + 64 / NOISE_FIN_W - 1) / (64 / NOISE_FIN_W), NOISE_GRID_CAP));
   RecHdr *hdr_w = const_cast<RecHdr *>(hdr);
 #define NOISE_DESC_TILES()                                                     \
@@ -1013,25 +969,6 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
 #define NOISE_DESC_TILE(C, LEN)                                                \
   a.cls = C;                                                                   \
   hipLaunchKernelGGL((k_aead_tile<DECRYPT, LEN, false, kTileDesc>), grid, bt, 0, ax.aux, a);
-  if (DECRYPT && use_units) {
-    // companion: the small tile classes and the generic kernel; caller: the
-    // long records as units (unit_kernel.hpp), after k_seg_prep
-    NOISE_DESC_TILES()
-    if ((e = hipEventRecord(ax.join, ax.aux)) != hipSuccess) return e;
-    UnitArgs ua;
-    ua.in = in;
-    ua.out = out;
-    ua.status = status;
-    ua.rt = ta.rt;
-    ua.fin = fin;
-    ua.finl = finl;
-    ua.bucket_cnt = hdr->counts + kColFin0;
-    ua.nlong = &hdr->nlong;
-    const dim3 gunit(capped(nrec, NOISE_UNIT_GRID));
-    hipLaunchKernelGGL(k_unit_dec, gunit, dim3(kUnitThreads), 0, stream, ua);
-    if ((e = hipStreamWaitEvent(stream, ax.join, 0)) != hipSuccess) return e;
-    return hipGetLastError();
-  }
   if (!DECRYPT) {
     // companion: dense tile classes first, the long-latency tails last (they
     // then overlap the segment kernel's drain; tails first: -3..5 %)
@@ -1127,8 +1064,7 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   const uint64_t o_idx = align_up(o_wbase + nw * kCols * 8, 256);
   const uint64_t o_tails = align_up(o_idx + nrec * 4, 256);
   const uint64_t o_fin = align_up(o_tails + nrec * 4, 256);
-  const uint64_t o_finl = align_up(o_fin + nrec * 4, 256);
-  const uint64_t o_rt = align_up(o_finl + nrec * 4, 256);
+  const uint64_t o_rt = align_up(o_fin + nrec * 4, 256);
   const uint64_t o_segs = align_up(o_rt + nrec * sizeof(SegRec), 256);
   const uint64_t o_part2 = align_up(o_segs + segcap * sizeof(SegEntry), 256);
   const uint64_t o_phi = align_up(o_part2 + segcap * sizeof(SegPartial), 256);
@@ -1143,7 +1079,6 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   uint32_t *idx = reinterpret_cast<uint32_t *>(base + o_idx);
   uint32_t *tails = reinterpret_cast<uint32_t *>(base + o_tails);
   uint32_t *fin = reinterpret_cast<uint32_t *>(base + o_fin);
-  uint32_t *finl = reinterpret_cast<uint32_t *>(base + o_finl);
   SegRec *rt = reinterpret_cast<SegRec *>(base + o_rt);
   SegEntry *segs = reinterpret_cast<SegEntry *>(base + o_segs);
   SegPartial *partial = reinterpret_cast<SegPartial *>(base + o_part2);
@@ -1152,7 +1087,7 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   const dim3 b64(64);
   hipLaunchKernelGGL(k_cls_count, dim3((unsigned)nw), b64, 0, stream, recs, nrec, (uint32_t)chunk, keys, nkeys, in, out, part);
   hipLaunchKernelGGL(k_cls_scan, dim3(kCols), b64, 0, stream, part, (uint32_t)nw, wbase, hdr, segcap);
-  hipLaunchKernelGGL(k_cls_scatter, dim3((unsigned)nw), b64, 0, stream, recs, nrec, (uint32_t)chunk, keys, nkeys, in, out, wbase, hdr, idx, rt, segs, tails, fin, finl, segcap);
+  hipLaunchKernelGGL(k_cls_scatter, dim3((unsigned)nw), b64, 0, stream, recs, nrec, (uint32_t)chunk, keys, nkeys, in, out, wbase, hdr, idx, rt, segs, tails, fin, segcap);
 
   TileArgs ta{};
   ta.in = in;
@@ -1172,19 +1107,10 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   // the decrypt pipeline's chunks pay off on large batches only (each chunk
   // adds four launches and a stream hand-off)
   const int chunks = nrec >= kChunkMinRecords ? kSegChunks : 1;
-  return decrypt ? launch_classes<true>(ta, nrec, hdr, keys, nkeys, recs, idx, tails, fin, finl, segcap,
+  return decrypt ? launch_classes<true>(ta, nrec, hdr, keys, nkeys, recs, idx, tails, fin, segcap,
                                        in, out, ad, status, stream, chunks)
-                 : launch_classes<false>(ta, nrec, hdr, keys, nkeys, recs, idx, tails, fin, finl, segcap,
+                 : launch_classes<false>(ta, nrec, hdr, keys, nkeys, recs, idx, tails, fin, segcap,
                                          in, out, ad, status, stream, 1);
 }
 
-#if defined(NOISE_UNIT_STAMPS)
-// timing builds: the unit kernel's per-phase sums (tools/unit_ab.py), reset
-extern "C" int noise_amd_unit_stamps(unsigned long long out[8]) {
-  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_unit_ts), 8 * sizeof(unsigned long long));
-  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_unit_ts), z, sizeof z);
-  return e == hipSuccess ? 0 : 1;
-}
-#endif
 }  // namespace noise_amd

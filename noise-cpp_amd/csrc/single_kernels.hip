@@ -117,28 +117,6 @@ __device__ __forceinline__ F26 add26(const F26 &a, const F26 &b) {
   return r;
 }
 
-// tools/ubench/one_timing.hip and resident_timing.hip build this file with
-// NOISE_ONE_TIMING: s_memrealtime stamps at the phase boundaries go to LDS
-// (a store to the host image would put a PCIe write into the next vmcnt
-// wait) and are copied to the last 64 bytes of the host image afterwards
-// (kOneTsOff): by one_finish before the done word (launch path), after the
-// speculation (resident).
-#ifdef NOISE_ONE_TIMING
-__shared__ uint64_t g_one_ts[8];
-#define NOISE_ONE_STAMP(i) \
-  if (threadIdx.x == 0) g_one_ts[i] = __builtin_amdgcn_s_memrealtime()
-#define NOISE_FAST_STAMP(i) \
-  if (threadIdx.x == 64) g_one_ts[i] = __builtin_amdgcn_s_memrealtime()
-constexpr uint64_t kOneTsOff = one_layout(kOneMaxAd, 65535u).total - 64u;
-#define NOISE_TS_FLUSH(b)                                                        \
-  if (threadIdx.x == 0)                                                          \
-    for (int i_ = 0; i_ < 8; ++i_) reinterpret_cast<uint64_t *>((b) + kOneTsOff)[i_] = g_one_ts[i_]
-#else
-#define NOISE_ONE_STAMP(i) ((void)0)
-#define NOISE_FAST_STAMP(i) ((void)0)
-#define NOISE_TS_FLUSH(b) ((void)0)
-#endif
-
 // Step 5 of every single-record body: the resident kernel's request image
 // is zeroed (the key words of the request line -- its sequence words stay --
 // and the npc staged input pieces), then every store of the workgroup is
@@ -156,15 +134,10 @@ __device__ __forceinline__ void one_finish(const OneArgs &a, const OneLayout &la
       for (uint32_t i = t; i < npc; i += kOneBlock) st_sys16(a.in_base, lay.ad + 16ull * i, z);
     req_wipe(a, t, kOneBlock);
   }
-#ifdef NOISE_ONE_SYSFENCE  // A/B (tools/ubench/one_timing): the full system release
-  __threadfence_system();
-#endif
 #if defined(__HIP_DEVICE_COMPILE__)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
   __syncthreads();
-  NOISE_ONE_STAMP(5);
-  if (!a.wipe_in) NOISE_TS_FLUSH(a.base);  // launch path (one_timing)
   if (t == 0)
     __hip_atomic_store(reinterpret_cast<uint32_t *>(a.base), a.seq, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
@@ -180,7 +153,6 @@ __device__ __forceinline__ void one_finish(const OneArgs &a, const OneLayout &la
 template <bool DECRYPT_T, bool RT = false>
 __device__ __forceinline__ void one_body(const OneArgs &a, uint4 *lds) {
   const bool DECRYPT = RT ? a.dec != 0u : DECRYPT_T;
-  NOISE_ONE_STAMP(0);
   const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
   const uint32_t L = a.len, A = a.ad_len;
   const uint32_t na = (A + 15u) >> 4, nl = (L + 15u) >> 4;
@@ -216,7 +188,6 @@ __device__ __forceinline__ void one_body(const OneArgs &a, uint4 *lds) {
       chacha20_block(a.key.w, b, nlo, nhi, ks[j]);
     }
   }
-  NOISE_ONE_STAMP(1);
   wait_vmem();  // this wave's DMA has landed ...
   __syncthreads();  // ... and every other wave's
   // quad: thread (b, q) holds keystream words 4r + q (r = 0..3) of block b,
@@ -269,7 +240,6 @@ __device__ __forceinline__ void one_body(const OneArgs &a, uint4 *lds) {
   }
   __syncthreads();
 
-  NOISE_ONE_STAMP(2);
   // 3. Poly1305 tree over P = na + nl + 1 blocks
   const uint32_t P = na + nl + 1u;
   const uint32_t NW = P > 256u ? 4u : 1u;  // waves taking part
@@ -380,7 +350,6 @@ __device__ __forceinline__ void one_body(const OneArgs &a, uint4 *lds) {
   }
   __syncthreads();
 
-  NOISE_ONE_STAMP(3);
   // 4. LDS -> staging
   uint32_t *hdr = reinterpret_cast<uint32_t *>(base);
   if (!DECRYPT) {
@@ -424,7 +393,6 @@ __device__ __forceinline__ void one_body(const OneArgs &a, uint4 *lds) {
       __hip_atomic_store(hdr + 1, ok ? NOISE_GPU_REC_OK : NOISE_GPU_REC_BAD_MAC, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  NOISE_ONE_STAMP(4);
   one_finish(a, lay, na + nl + (DECRYPT ? 1u : 0u));
 }
 
@@ -668,7 +636,6 @@ __device__ void one_body_fast(const OneArgs &a, uint4 *lds, const SpecSlot *sp, 
   }
   const uint32_t u = t - 64u;
   grp_wait(gc, 1u);
-  NOISE_FAST_STAMP(1);
   const uint32_t P = na + nl + 1u;
   F26 h;
 #pragma unroll
@@ -733,7 +700,6 @@ __device__ void one_body_fast(const OneArgs &a, uint4 *lds, const SpecSlot *sp, 
     grp_arrive1(gc);  // -> 5
   }
   grp_wait(gc, 5u);
-  NOISE_FAST_STAMP(3);
   // LDS -> host image
   if (!DECRYPT) {
     if (u <= nl) {  // ct pieces, then the tag
@@ -757,7 +723,6 @@ __device__ void one_body_fast(const OneArgs &a, uint4 *lds, const SpecSlot *sp, 
                          ok ? NOISE_GPU_REC_OK : NOISE_GPU_REC_BAD_MAC, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  NOISE_FAST_STAMP(4);
   // the request image zeroed (but for the seq words), every store drained,
   // then the done word (as one_finish, over waves 1..3)
   {
@@ -771,7 +736,6 @@ __device__ void one_body_fast(const OneArgs &a, uint4 *lds, const SpecSlot *sp, 
   grp_arrive(gc, lane);  // -> 8
   if (t == 64) {
     grp_wait(gc, 8u);
-    NOISE_FAST_STAMP(5);
     __hip_atomic_store(reinterpret_cast<uint32_t *>(a.base), a.seq, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -806,6 +770,8 @@ __device__ __forceinline__ void ld_sys16x2(const uint8_t *p, u32x4 &c0, u32x4 &c
 #endif
 }
 
+constexpr uint32_t kResSleepPolls = 4096u;  // empty polls before the wave backs off
+
 // LDS: the staging image (one_lds_bytes(kOneMaxAd, 65535)), the
 // speculation tables and slots, the request broadcast, the next block 0, the
 // group counter
@@ -838,41 +804,34 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_resident(uint8_t *req, uint8
   __syncthreads();
   for (;;) {
     if (t < 64) {  // wave 0 polls chunks lane and 64 + lane (header: chunks 0..3)
-      uint32_t ex = 0, polls = 0, n_inl = 0;
+      uint32_t ex = 0, polls = 0, n_inl = 0, dseq = 0;
       u32x4 c = {0u, 0u, 0u, 0u}, c1 = {0u, 0u, 0u, 0u};
       for (;;) {
         ld_sys16x2(req + 16u * lane, c, c1);
-        const uint32_t seq = (uint32_t)__shfl((int)c.x, 0);
-        const uint64_t same = __ballot(lane < 4 && c.x == seq);
+        // each chunk's seq, decoded with its own payload words (launchers.hpp
+        // req_chunk_tag): a chunk that landed in part decodes to something
+        // else.  Per lane and folded into the compares below -- no cross-lane
+        // sum on the accept path.
+        dseq = c.x ^ req_chunk_tag(lane, c.y, c.z, c.w);
+        const uint32_t dseq1 = c1.x ^ req_chunk_tag(64u + lane, c1.y, c1.z, c1.w);
+        const uint32_t seq = (uint32_t)__builtin_amdgcn_readfirstlane((int)dseq);
+        const uint64_t same = __ballot(lane < 4 && dseq == seq);
         if (seq != last && (same & 0xfull) == 0xfull) {
           // a complete header; an inline record must be complete too (every
-          // chunk carries this seq), else poll again
-          const uint32_t meta = (uint32_t)__shfl((int)c.y, 0);
+          // chunk decodes to this seq), else poll again
+          const uint32_t meta = (uint32_t)__builtin_amdgcn_readfirstlane((int)c.y);
           n_inl = req_inline_chunks((meta >> 16) & 0x3fffu, meta & 0xffffu, (meta >> 30) & 1u);
           const bool need0 = lane >= 4u && lane - 4u < n_inl, need1 = 60u + lane < n_inl;
-          if (__ballot((need0 && c.x != seq) || (need1 && c1.x != seq)) == 0ull) {
-            // every chunk carries seq; the words must also sum to the check
-            // word (launchers.hpp req_check_mix), else a chunk landed in part
-            // (DPP row sums + 4 readlanes: a chain of LDS-crossbar shuffles
-            // here cost ~0.5 us per request)
-            uint32_t v = 0u;
-            if (lane < 4u || need0) v = req_check_mix(lane, c.y, c.z, lane == 3u ? 0u : c.w);
-            if (need1) v += req_check_mix(64u + lane, c1.y, c1.z, c1.w);
-            v = rows_total(row_sum_dpp(v));
-            if (v + kReqCheckSalt == (uint32_t)__builtin_amdgcn_readlane((int)c.w, 3)) {
-              NOISE_ONE_STAMP(0);
-              break;
-            }
+          if (__ballot((need0 && dseq != seq) || (need1 && dseq1 != seq)) == 0ull) {
+            break;
           }
         }
-#ifndef NOISE_RES_SLEEP_POLLS  // empty polls before the wave starts to s_sleep between polls
-#define NOISE_RES_SLEEP_POLLS 4096u
-#endif
-        // a long-idle instance backs off (s_sleep 32: ~2048 clocks, about one
+        // a long-idle instance backs off after kResSleepPolls (4096, ~1 ms)
+        // empty polls (s_sleep 32: ~2048 clocks, about one
         // more poll round trip, between polls): half the poll traffic and
         // issue slots; a request that follows the previous one within a few
         // ms is still seen at the full poll rate
-        if (polls >= NOISE_RES_SLEEP_POLLS) __builtin_amdgcn_s_sleep(32);
+        if (polls >= kResSleepPolls) __builtin_amdgcn_s_sleep(32);
         if ((++polls & 31u) == 0u) {
           // ONE decision for the wave (lane 0's).  On the GPU the stop word
           // is one load instruction and the clock a scalar read, so the lanes
@@ -913,10 +872,9 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_resident(uint8_t *req, uint8
         cmd[4 * lane + 3] = c.w;
       }
       if (lane == 0) {
-        cmd[0] = ex ? 0u : c.x;  // 0: leave
+        cmd[0] = ex ? 0u : dseq;  // the decoded seq; 0: leave
         cmd[16] = n_inl;
       }
-      NOISE_ONE_STAMP(2);
     }
     __syncthreads();
     const uint32_t n_inl = cmd[16];
@@ -970,7 +928,6 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_resident(uint8_t *req, uint8
     const uint32_t nks = nb < 16u ? 16u : (nb > kSpecBlocks - 1u ? kSpecBlocks - 1u : nb);
     const uint32_t pmax = P <= 80u ? 80u : (P <= 128u ? 128u : kFastMaxBlocks);
     SpecBuf *nbuf = &bufs[spare];
-    NOISE_ONE_STAMP(7);
     if (hit >= 0 && P <= kFastMaxBlocks) {
       // waves 1..3 serve, wave 0 starts the next speculation meanwhile
       one_body_fast<false, true>(a, lds, &slots[hit], &bufs[slots[hit].buf], nbuf, pmax, pre, sync);
@@ -989,8 +946,6 @@ __global__ __launch_bounds__(kOneBlock) void k_aead_resident(uint8_t *req, uint8
     last = seq;
     __syncthreads();
     spec_finish(&slots[dst], spare, nbuf, pre, sync, a.key.w, a.nonce + 1u, ++stamp, nks, pmax);
-    NOISE_ONE_STAMP(6);
-    NOISE_TS_FLUSH(base);  // this request's stamps, read by the host during the next one
 #pragma unroll
     for (int i = 0; i < 8; ++i) a.key.w[i] = 0u;
     t_last = __builtin_amdgcn_s_memrealtime();

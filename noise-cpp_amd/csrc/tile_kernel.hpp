@@ -87,13 +87,6 @@ __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// A/B knob (round 5): the Poly1305 pass's DMAs with the default policy
-#ifdef NOISE_POLY_DMA_PLAIN
-constexpr bool kPolyDmaPlain = true;
-#else
-constexpr bool kPolyDmaPlain = false;
-#endif
-
 // Record addressing / keying of a tile launch.
 enum TileMode : int {
   kTileUniform = 0,   // one key, nonce0 + i, record i at in + i*in_stride
@@ -120,7 +113,7 @@ enum TileMode : int {
 // (Horner in R = r^64), appends the tail (k_seg_tail: the len % 1024 bytes
 // past the last full segment, one lane per tail) as h r^(tail blocks) +
 // P_tail, then the length block and the tag.
-struct SegRec {                  // one per long record, 384 B (three 128-B lines)
+struct SegRec {                  // one per long record, 256 B (two 128-B lines)
   uint64_t in_off, out_off, nonce, seg0;  // seg0: index of segment 0
   uint32_t k[8];                 // the record's key (copied from the key table)
   uint32_t key_idx, di, len, nfull;       // di: descriptor index
@@ -132,11 +125,8 @@ struct SegRec {                  // one per long record, 384 B (three 128-B line
   uint32_t ok;                   // decrypt: 1 once the finalize kernel verified the tag
   uint32_t pw8[5];               // r^8 (radix 2^26): the 128-B span passes
   uint32_t pad[5];
-  // decrypt (unit_kernel.hpp): R^2, R^4, R^8, R^16, R^32 for R = r^64 (radix 2^26)
-  uint32_t rpow[5][5];
-  uint32_t pad2[7];
 };
-static_assert(sizeof(SegRec) == 384, "SegRec layout");
+static_assert(sizeof(SegRec) == 256, "SegRec layout");
 struct SegEntry {                // one per full segment
   uint32_t q, s;                 // long-record index, segment number
 };
@@ -201,9 +191,11 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
   using C = TileCfg<L, SPAN>;
   if (ABL == 1) return;
   constexpr bool TAGGED_IN = DECRYPT && MODE < kTileSeg;  // ct || tag pieces
-  // every record byte is read once (nt), except that the decrypt's Poly1305
-  // pass reads the ciphertext the keystream pass reads again
-  constexpr bool NT = !(MODE == kTileSegPoly && kPolyDmaPlain);
+  // every record byte is read once: the streaming (nt) policy.  (Round 5:
+  // the default policy on the decrypt's Poly1305 pass, whose ciphertext the
+  // keystream pass reads again, was no faster at 4, 16, 32 or 64 chunks --
+  // profiles/round5/ab/cfg4_chunks_policy.txt.)
+  constexpr bool NT = true;
   constexpr int IN_SLOTS = TAGGED_IN ? C::NSLOT : C::REC_SLOTS;
   if (CONTIG) {
     // slot s = 64q + lane holds piece swz(s) = 64q + glq(gl, q); packed

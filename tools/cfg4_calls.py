@@ -1,7 +1,8 @@
 """Timing-only A/B of the records path on BASELINE config 4's batch (no
-correctness check: ablation builds produce wrong bytes on purpose).
-    NOISE_AMD_LIB=ab/x.so python tools/unit_ab.py [reps]
-Prints the median encrypt / decrypt call time (HIP events on the stream)."""
+correctness check: ablation builds may produce wrong bytes on purpose).
+    NOISE_AMD_LIB=ab/x.so python tools/cfg4_calls.py [reps]
+Prints the median encrypt / decrypt call time (HIP events on the stream).
+Round 5 used it for the unit-kernel A/Bs (profiles/round5/ab/cfg4_units.md)."""
 import os
 import sys
 import types
@@ -32,20 +33,6 @@ def main():
     dec.sort()
     print("%s enc %.4f dec %.4f ms" % (os.path.basename(os.environ.get("NOISE_AMD_LIB", "in-tree")),
                                       enc[reps // 2], dec[reps // 2]))
-    lib = bench.noise_amd.load()
-    if hasattr(lib, "noise_amd_unit_stamps"):  # NOISE_UNIT_STAMPS builds: per-phase wave time
-        import ctypes
-        out = (ctypes.c_ulonglong * 8)()
-        lib.noise_amd_unit_stamps(out)  # reset
-        wl["step"]()
-        torch.cuda.synchronize()
-        lib.noise_amd_unit_stamps(out)
-        units = out[7]
-        names = ["A+dma wait", "C poly", "barrier", "D tags", "E keystream", "F wait", "F stores+dma"]
-        tot = sum(out[:7])
-        print("  units %d (x4 waves); per wave-unit us: " % units +
-              ", ".join("%s %.2f (%.0f%%)" % (n, out[i] / 100.0 / max(units, 1), 100.0 * out[i] / max(tot, 1))
-                        for i, n in enumerate(names)))
 
 
 if __name__ == "__main__":

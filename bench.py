@@ -864,6 +864,14 @@ def roofline(cfg, wl, enc_ms, dec_ms):
                 "frac": round(vi / (kms * 1e-3) / VALU_PEAK, 4),
                 "issue_model": "1024 SIMDs x 2.4 GHz / 4 cycles per wave64 instruction (measured cost "
                                "of every instruction in a ChaCha/Poly1305 stream on gfx950)"}
+        # the HBM fraction the VALU work alone allows: the launch cannot be
+        # shorter than its instructions at the issue model's rate, so its
+        # bytes cannot move faster than bytes / (VALU / peak issue rate)
+        cap = kbytes * VALU_PEAK / (vi * HBM_PEAK) if vi else None
+        valu["hbm_frac_cap"] = round(cap, 4) if cap else None
+        valu["hbm_frac_cap_note"] = ("bytes per launch / (VALU per launch / %.1f G/s) / 8 TB/s: the rw "
+                                     "fraction reachable at 100 %% VALU issue" % (VALU_PEAK / 1e9))
+        roof["valu_cap_hbm_frac"] = valu["hbm_frac_cap"]
         if "SQ_WAVES" in pmc and pmc["SQ_WAVES"]:
             valu["insts_per_wave"] = int(pmc["SQ_INSTS_VALU"] / pmc["SQ_WAVES"])
         if pmc.get("GRBM_GUI_ACTIVE"):

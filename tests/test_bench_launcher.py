@@ -122,3 +122,9 @@ def test_roofline_fields_from_committed_profiles(cfg):
         assert 0 < roof["hbm_frac_read"] < roof["hbm_frac_rw"] < 1
         v = roof["valu"]
         assert v["insts_per_wave"] > 10000 and 0 < v["frac"] <= 1.2 and 0 < v["issue_util_profiled"] <= 1.05
+        # the VALU-implied cap on the HBM fraction: above the achieved one
+        # (the kernel cannot beat its own instruction count), below 1, and
+        # the achieved fraction over it is the VALU issue fraction
+        cap = roof["valu_cap_hbm_frac"]
+        assert roof["hbm_frac_rw"] < cap < 1.0
+        assert abs(roof["hbm_frac_rw"] / cap - v["frac"]) < 0.01

@@ -52,11 +52,16 @@ constexpr int kCols = kNumCls + 2 + kFinBuckets;
 // Decrypt pipelines the long records in kSegChunks chunks (launch_classes):
 // the Poly1305 pass of chunk c + 1 (HBM-bound) runs beside the keystream pass
 // of chunk c (VALU-bound).  Chunk boundaries fall on record starts, near
-// (2c - 1) nseg / (2 kSegChunks - 1) segments (chunk 0 half the others).
+// (1 + (c - 1) W) nseg / (1 + (kSegChunks - 1) W) segments (chunk 0 1/W of
+// the others, W = kChunkW).
 #ifndef NOISE_SEG_CHUNKS
 #define NOISE_SEG_CHUNKS 4
 #endif
 constexpr int kSegChunks = NOISE_SEG_CHUNKS;
+#ifndef NOISE_CHUNK_W
+#define NOISE_CHUNK_W 2
+#endif
+constexpr unsigned long long kChunkW = NOISE_CHUNK_W;  // chunk c >= 1 : chunk 0
 #ifndef NOISE_CHUNK_MIN  // overridable for the CPU emulation build
 #define NOISE_CHUNK_MIN 65536
 #endif
@@ -73,9 +78,12 @@ constexpr int kHdrWords = kSegChunks <= 4 ? 64 : 256;    // scratch header: 512 
 #ifndef NOISE_XOR_SPAN
 #define NOISE_XOR_SPAN 128
 #endif
-// The Poly1305 pass's span per lane (r^8 from the SegRec at 128 B)
+// The Poly1305 pass's span per lane: 256 B, as the encrypt segment kernel
+// (one recombination product per lane with the SegRec's powers; 128-B spans
+// would need r^8 .. r^56).  Round 5, per-kernel PMC: 53 M VALU per chunk
+// against 79 M for 128-B spans with a three-product recombination.
 #ifndef NOISE_POLY_SPAN
-#define NOISE_POLY_SPAN 128
+#define NOISE_POLY_SPAN 256
 #endif
 #ifndef NOISE_CLASSIFY_MIN  // overridable for the CPU emulation build
 #define NOISE_CLASSIFY_MIN 2048
@@ -366,9 +374,9 @@ __global__ __launch_bounds__(64) void k_cls_scatter(
       const unsigned long long total = hdr->counts[kColSegs];
 #pragma unroll
       for (int k = 1; k < kSegChunks; ++k) {  // the record holding a chunk's first segment
-        // chunk 0 half the size of the others (1 : 2 : 2 : ...): the first
-        // tag check, and so the keystream pass, can start sooner
-        const unsigned long long b = total * (2ull * k - 1ull) / (2ull * kSegChunks - 1ull);
+        // chunk 0 smaller than the others (1 : W : W : ...): the first tag
+        // check, and so the keystream pass, can start sooner
+        const unsigned long long b = total * (1ull + (k - 1ull) * kChunkW) / (1ull + (kSegChunks - 1ull) * kChunkW);
         if (seg0 <= b && b < seg0 + nf) {
           hdr->qsplit[k] = q;
           hdr->ssplit[k] = seg0;
@@ -402,8 +410,8 @@ __global__ __launch_bounds__(64) void k_cls_scatter(
 
 // ---- 2. long records --------------------------------------------------------
 // k_seg_prep: lane per long record -> ChaCha block 0 (one-time key r, s),
-// r^16, r^32 (the segment kernel's 4-lane recombination) and r^64 (the
-// finalize kernel's Horner step over segments).
+// r^16, r^32, r^48 (the segment passes' per-lane recombination) and r^64
+// (the finalize kernel's Horner step over segments).
 __global__ __launch_bounds__(64) void k_seg_prep(const uint8_t *__restrict__ keys,
                                                  SegRec *rt, const RecHdr *hdr) {
   const uint64_t n = hdr->nlong;
@@ -425,14 +433,13 @@ __global__ __launch_bounds__(64) void k_seg_prep(const uint8_t *__restrict__ key
     // squaring chain r^(2^b); r^(tail blocks) = product over the bits of
     // the tail's Poly1305 block count (1..64)
     const uint32_t nbt = ((R.len & 1023u) + 15u) >> 4;
-    F26 x = to26(r0, r1, r2, r3, 0u), rt_pow, x8;
+    F26 x = to26(r0, r1, r2, r3, 0u), rt_pow;
     rt_pow.a[0] = 1u;
     rt_pow.a[1] = rt_pow.a[2] = rt_pow.a[3] = rt_pow.a[4] = 0u;
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       if ((nbt >> b) & 1u) rt_pow = mul26(rt_pow, x);
       x = mul26(x, x);
-      if (b == 2) x8 = x;  // r^8
     }
     // x = r^16
     if ((nbt >> 4) & 1u) rt_pow = mul26(rt_pow, x);
@@ -441,11 +448,14 @@ __global__ __launch_bounds__(64) void k_seg_prep(const uint8_t *__restrict__ key
     if ((nbt >> 6) & 1u) rt_pow = mul26(rt_pow, x64);  // a 1009..1023-byte tail: 64 blocks
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
-      R.pw8[i] = x8.a[i];
-      R.pw16[i] = x.a[i];
-      R.pw32[i] = x32.a[i];
       R.r64[i] = x64.a[i];
       R.rtail[i] = rt_pow.a[i];
+    }
+    const F26 pw[3] = {x, x32, mul26(x32, x)};
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      *reinterpret_cast<u32x4 *>(R.pwlo[m]) = u32x4{pw[m].a[0], pw[m].a[1], pw[m].a[2], pw[m].a[3]};
+      R.pwhi[m] = pw[m].a[4];
     }
   }
 }
@@ -929,6 +939,8 @@ static hipError_t aux_release(int dev, hipStream_t stream) {
 //   companion  : (wait prep) tail Poly1305 -> join, small classes, generic,
 //                then per chunk (wait fin[c]) the chunk's tail plaintext -> join2
 //   companion 2: per chunk (wait fin[c]) XOR(c) -> xdone
+// (A third companion for the tails' plaintext, so that it does not queue
+// behind the small classes, measured 1-2 % slower: round 5.)
 template <bool DECRYPT>
 static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr *hdr,
                                  const uint8_t *keys, uint32_t nkeys,

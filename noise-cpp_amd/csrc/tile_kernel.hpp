@@ -119,11 +119,14 @@ struct SegRec {                  // one per long record, 256 B (two 128-B lines)
   uint32_t key_idx, di, len, nfull;       // di: descriptor index
   uint32_t r[4];                 // clamped Poly1305 r (radix 2^32)
   uint32_t s[4];                 // Poly1305 s
-  uint32_t pw16[5], pw32[5], r64[5];      // r^16, r^32, r^64 (radix 2^26)
+  // r^16, r^32, r^48 (radix 2^26; limbs 0..3 | limb 4): lane j of a
+  // segment's four 256-B spans scales its Horner sum by r^(16 (3 - j)) with
+  // ONE product from its own load (the tile kernel's kTileSeg* modes)
+  uint32_t pwlo[3][4], pwhi[3];
+  uint32_t r64[5];               // r^64 (radix 2^26)
   uint32_t rtail[5];             // r^(tail blocks) (radix 2^26)
   uint32_t ptail[5];             // the tail's Poly1305 sum (radix 2^32, h4 small)
   uint32_t ok;                   // decrypt: 1 once the finalize kernel verified the tag
-  uint32_t pw8[5];               // r^8 (radix 2^26): the 128-B span passes
   uint32_t pad[5];
 };
 static_assert(sizeof(SegRec) == 256, "SegRec layout");
@@ -301,8 +304,8 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
 // kTileSeg*: the per-lane metadata of one segment (from its SegRec); each
 // pass loads only what it uses (the Poly1305 pass no key, the XOR pass no r)
 struct SegMeta {
-  uint32_t k[8], r[4], pw8[5], pw16[5], pw32[5];
-  uint32_t nlo, nhi, in_lo, in_hi, out_lo, out_hi, cb, ok, inpl;
+  uint32_t k[8], r[4];
+  uint32_t nlo, nhi, in_lo, in_hi, out_lo, out_hi, cb, ok, inpl, q;
 };
 template <int MODE, int SPAN>
 __device__ __forceinline__ void seg_meta_load(SegMeta &m, const SegRec *rt, const SegEntry e,
@@ -312,11 +315,10 @@ __device__ __forceinline__ void seg_meta_load(SegMeta &m, const SegRec *rt, cons
   for (int i = 0; i < 8; ++i) m.k[i] = 0u;
 #pragma unroll
   for (int i = 0; i < 4; ++i) m.r[i] = 0u;
-#pragma unroll
-  for (int i = 0; i < 5; ++i) m.pw8[i] = m.pw16[i] = m.pw32[i] = i == 0 ? 1u : 0u;
-  m.nlo = m.nhi = m.in_lo = m.in_hi = m.out_lo = m.out_hi = m.cb = m.ok = m.inpl = 0u;
+  m.nlo = m.nhi = m.in_lo = m.in_hi = m.out_lo = m.out_hi = m.cb = m.ok = m.inpl = m.q = 0u;
   if (valid) {
     const SegRec &R = rt[e.q];
+    m.q = e.q;
     const uint64_t io = R.in_off + 1024ull * e.s, oo = R.out_off + 1024ull * e.s;
     m.in_lo = (uint32_t)io; m.in_hi = (uint32_t)(io >> 32);
     m.out_lo = (uint32_t)oo; m.out_hi = (uint32_t)(oo >> 32);
@@ -329,12 +331,6 @@ __device__ __forceinline__ void seg_meta_load(SegMeta &m, const SegRec *rt, cons
     if (POLY) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) m.r[i] = R.r[i];
-#pragma unroll
-      for (int i = 0; i < 5; ++i) {
-        if (SPAN == 128) m.pw8[i] = R.pw8[i];
-        m.pw16[i] = R.pw16[i];
-        m.pw32[i] = R.pw32[i];
-      }
     }
     if (MODE == kTileSegXor) {
       m.ok = R.ok;
@@ -371,6 +367,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
   static_assert(!(CONTIG && (MODE == kTileDesc || SEG)), "descriptor tiles are strided");
   static_assert(!SEG || (L == 1024 && (SPAN == 256 || SPAN == 128)),
                 "segments are 1 KiB, 256 or 128 B per lane");
+  static_assert(!SEG || !DO_POLY || SPAN == 256, "the SegRec holds the 256-B spans' powers");
   static_assert(NBUF == 1 || NBUF == 2, "one or two tile buffers");
   // the Poly1305 pass issues the next tile's DMA into buffer 0 itself
   static_assert(MODE != kTileSegPoly || NBUF == 1, "the Poly1305 pass has one tile buffer");
@@ -408,7 +405,8 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
        super0 += (uint64_t)gridDim.x * 64) {
   // ---- key pass: lane l -> one-time key of record super0 + l -------------
   uint32_t kr[4], kss[4];
-  F26 pw[C::LOG2G > 0 ? C::LOG2G : 1];
+  F26 pw[C::LOG2G > 0 && !SEG ? C::LOG2G : 1];  // uniform / keyed: r^BPL, r^(2 BPL), ...
+  uint32_t own_q = 0;  // kTileSeg*: the long record of segment super0 + lane
   uint32_t own_k[8], own_nlo = 0, own_nhi = 0;  // keyed modes: this lane's record
   uint32_t own_in_lo = 0, own_in_hi = 0, own_out_lo = 0, own_out_hi = 0, own_di = 0;
   uint32_t own_cb = 0;  // kTileSeg: first ChaCha block counter - 1 (16 s)
@@ -423,17 +421,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     for (int i = 0; i < 8; ++i) own_k[i] = nxt.k[i];
 #pragma unroll
     for (int i = 0; i < 4; ++i) { kr[i] = nxt.r[i]; kss[i] = 0u; }
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {  // r^BPL, r^(2 BPL), ...: 16, 32 (256-B spans) or 8, 16, 32 (128)
-      if (SPAN == 128) {
-        pw[0].a[i] = nxt.pw8[i];
-        pw[C::LOG2G > 1 ? 1 : 0].a[i] = nxt.pw16[i];
-        pw[C::LOG2G > 2 ? 2 : 0].a[i] = nxt.pw32[i];
-      } else {
-        pw[0].a[i] = nxt.pw16[i];
-        pw[C::LOG2G > 1 ? 1 : 0].a[i] = nxt.pw32[i];
-      }
-    }
+    own_q = nxt.q;
     own_nlo = nxt.nlo;
     own_nhi = nxt.nhi;
     own_in_lo = nxt.in_lo; own_in_hi = nxt.in_hi;
@@ -531,6 +519,18 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     else wait_vmem();
     wave_lds_fence();
     if (SEG && t == 0) seg_meta_load<MODE, SPAN>(nxt, a.rt, nxt_e, next0 + lane < nrec, in, out);
+    // kTileSeg*: this lane's recombination power r^(16 (3 - j)) from its
+    // segment's SegRec (lands during the Horner chain below; j = 3: 1)
+    F26 own_pw;
+    if (SEG && DO_POLY) {
+      const uint32_t qs = (uint32_t)__shfl((int)own_q, (int)((uint32_t)t * C::RPT + rho));
+      const uint32_t m = C::G - 1u - j, mi = m ? m - 1u : 0u;
+      const SegRec &R = a.rt[qs];
+      const uint4 v = *reinterpret_cast<const uint4 *>(R.pwlo[mi]);
+      const uint32_t v4 = R.pwhi[mi];
+      own_pw.a[0] = m ? v.x : 1u; own_pw.a[1] = m ? v.y : 0u; own_pw.a[2] = m ? v.z : 0u;
+      own_pw.a[3] = m ? v.w : 0u; own_pw.a[4] = m ? v4 : 0u;
+    }
     if (NBUF == 2 && t + 1 < C::G) {  // the next tile's DMA now, into the other buffer
       const uint64_t nrec0 = rec0 + C::RPT;
       if (nrec0 < nrec) {
@@ -615,17 +615,21 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     if (C::G > 1 && DO_POLY) {
       // acc_j * r^(BPL (G-1-j)), then sum over the record's G lanes
       F26 h = to26(p.h0, p.h1, p.h2, p.h3, p.h4);
-      const uint32_t m = C::G - 1 - j;
+      if (SEG) {
+        h = mul26(h, own_pw);
+      } else {
+        const uint32_t m = C::G - 1 - j;
 #pragma unroll
-      for (int b = 0; b < C::LOG2G; ++b) {
-        F26 f;
-        const bool use = (m >> b) & 1u;
+        for (int b = 0; b < C::LOG2G; ++b) {
+          F26 f;
+          const bool use = (m >> b) & 1u;
 #pragma unroll
-        for (int i = 0; i < 5; ++i) {
-          const uint32_t w = __shfl(pw[b].a[i], src);
-          f.a[i] = use ? w : (i == 0 ? 1u : 0u);
+          for (int i = 0; i < 5; ++i) {
+            const uint32_t w = __shfl(pw[b].a[i], src);
+            f.a[i] = use ? w : (i == 0 ? 1u : 0u);
+          }
+          h = mul26(h, f);
         }
-        h = mul26(h, f);
       }
 #pragma unroll
       for (int b = 0; b < C::LOG2G; ++b) {

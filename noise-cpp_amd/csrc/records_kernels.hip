@@ -85,6 +85,16 @@ constexpr int kHdrWords = kSegChunks <= 4 ? 64 : 256;    // scratch header: 512 
 #ifndef NOISE_POLY_SPAN
 #define NOISE_POLY_SPAN 256
 #endif
+// classifier geometry: waves (a multiple of 64) and the least records per wave
+#ifndef NOISE_CLS_WAVES
+#define NOISE_CLS_WAVES 4096  // round 5: 2048 waves of >= 512 ran 0.5 % slower per call
+#endif
+#ifndef NOISE_CLS_MIN_CHUNK
+#define NOISE_CLS_MIN_CHUNK 256
+#endif
+constexpr uint32_t kClsWaves = NOISE_CLS_WAVES;
+constexpr uint64_t kClsMinChunk = NOISE_CLS_MIN_CHUNK;
+static_assert(kClsWaves % 64 == 0 && kClsMinChunk % 64 == 0, "classifier geometry");
 #ifndef NOISE_CLASSIFY_MIN  // overridable for the CPU emulation build
 #define NOISE_CLASSIFY_MIN 2048
 #endif
@@ -234,7 +244,7 @@ __global__ __launch_bounds__(64) void k_cls_scan(const uint32_t *part, uint32_t 
                                                  unsigned long long *wbase,
                                                  RecHdr *hdr, uint64_t segcap) {
   const uint32_t lane = threadIdx.x, c = blockIdx.x;
-  constexpr uint32_t kPer = 32;  // nw <= 2048 (the classifier's geometry)
+  constexpr uint32_t kPer = kClsWaves / 64;  // nw <= kClsWaves (the classifier's geometry)
   const uint32_t w0 = lane * kPer;
   uint32_t v[kPer];
   unsigned long long tot = 0;  // 32 waves' segment counts can pass 2^32
@@ -1062,9 +1072,9 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   }
   if (nrec > 0xffffffffull) return hipErrorInvalidValue;  // 32-bit indices
 
-  // classifier geometry: at most 2048 waves of >= 512 records
-  uint64_t chunk = align_up((nrec + 2047) / 2048, 64);
-  if (chunk < 512) chunk = 512;
+  // classifier geometry: at most kClsWaves waves of >= kClsMinChunk records
+  uint64_t chunk = align_up((nrec + kClsWaves - 1) / kClsWaves, 64);
+  if (chunk < kClsMinChunk) chunk = kClsMinChunk;
   const uint64_t nw = (nrec + chunk - 1) / chunk;
   const uint64_t segcap = nrec * 63 < kSegCapMax ? nrec * 63 : kSegCapMax;
 

@@ -14,6 +14,6 @@ for d in sys.argv[1:]:
     print('==',d)
     tv=0;tc=0
     for k in sorted(acc):
-        if 'tile' not in k and 'seg' not in k and 'cls' not in k: continue
+        if not any(x in k for x in ('tile', 'seg', 'cls', 'unit')): continue
         v=acc[k]['SQ_INSTS_VALU']/n[k]; g=acc[k]['GRBM_GUI_ACTIVE']/n[k]/8
         print('%-50s valu %8.1fM cyc %8.0fk util %.3f'%(k[:50],v/1e6,g/1e3,v*4/1024/g if g else 0))

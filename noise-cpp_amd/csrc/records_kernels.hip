@@ -36,7 +36,6 @@
 #include "launchers.hpp"
 #include "noise_amd/dev_mem.hpp"
 #include "tile_kernel.hpp"
-#include "unit_kernel.hpp"
 
 namespace noise_amd {
 
@@ -48,7 +47,7 @@ constexpr int kNumCls = kNumTileCls + 2;
 constexpr int kColSegs = kNumCls;         // classifier column: full segments
 constexpr int kColTails = kNumCls + 1;    // classifier column: long records with a tail
 constexpr int kColFin0 = kNumCls + 2;     // classifier columns: long records by
-constexpr int kFinBuckets = kUnitBuckets; // unit bucket (unit_kernel.hpp), 0..5
+constexpr int kFinBuckets = 6;            // floor(log2(full segments)), 1..63 -> 0..5
 constexpr int kCols = kNumCls + 2 + kFinBuckets;
 // Decrypt pipelines the long records in kSegChunks chunks (launch_classes):
 // the Poly1305 pass of chunk c + 1 (HBM-bound) runs beside the keystream pass
@@ -96,16 +95,6 @@ constexpr int kHdrWords = kSegChunks <= 4 ? 64 : 256;    // scratch header: 512 
 constexpr uint32_t kClsWaves = NOISE_CLS_WAVES;
 constexpr uint64_t kClsMinChunk = NOISE_CLS_MIN_CHUNK;
 static_assert(kClsWaves % 64 == 0 && kClsMinChunk % 64 == 0, "classifier geometry");
-// decrypt's long records: 1 = units (k_unit_dec, one wave per unit of whole
-// records, Poly1305 -> tags -> keystream), 0 = the chunked segment passes
-#ifndef NOISE_DEC_UNITS
-#define NOISE_DEC_UNITS 1
-#endif
-constexpr bool kDecUnits = NOISE_DEC_UNITS != 0;
-// grid cap of the unit kernel (one-wave workgroups looping over the units)
-#ifndef NOISE_UNIT_GRID
-#define NOISE_UNIT_GRID NOISE_GRID_CAP
-#endif
 #ifndef NOISE_CLASSIFY_MIN  // overridable for the CPU emulation build
 #define NOISE_CLASSIFY_MIN 2048
 #endif
@@ -171,10 +160,10 @@ struct RecHdr {
 };
 static_assert(sizeof(RecHdr) == 8 * kHdrWords, "scratch header layout");
 
-// finalize-order bucket of a long record of `len` bytes: the unit bucket by
-// its items m = nfull + (tail != 0), floor(log2(m - 1)) (unit_kernel.hpp)
-__device__ __forceinline__ int fin_bucket(uint32_t len) {
-  return unit_bucket((len >> 10) + ((len & 1023u) != 0u ? 1u : 0u));
+// finalize-order bucket of a long record with nf >= 1 full segments
+__device__ __forceinline__ int fin_bucket(uint32_t nf) {
+  const int b = 31 - __builtin_clz(nf | 1u);
+  return b < kFinBuckets - 1 ? b : kFinBuckets - 1;
 }
 
 // wave-wide inclusive prefix sum (all 64 lanes participate)
@@ -221,11 +210,10 @@ __global__ __launch_bounds__(64) void k_cls_count(
   for (uint64_t i0 = b0; i0 < e0; i0 += 64) {
     const uint64_t i = i0 + lane;
     int cls = -1;
-    uint32_t nf = 0, d_len = 0;
+    uint32_t nf = 0;
     bool tail = false;
     if (i < e0) {
       const noise_gpu_record d = recs[i];
-      d_len = d.len;
       cls = record_class(d, keys, nkeys, in, out);
       nf = cls == kClsLong ? d.len >> 10 : 0u;
       tail = cls == kClsLong && (d.len & 1023u) != 0;
@@ -234,7 +222,7 @@ __global__ __launch_bounds__(64) void k_cls_count(
     for (int c = 0; c < kNumCls; ++c) cnt[c] += (uint32_t)__builtin_popcountll(__ballot(cls == c));
     nseg += wave_sum(nf);
     ntail += (uint32_t)__builtin_popcountll(__ballot(tail));
-    const int fb = cls == kClsLong ? fin_bucket(d_len) : -1;
+    const int fb = cls == kClsLong ? fin_bucket(nf) : -1;
 #pragma unroll
     for (int b = 0; b < kFinBuckets; ++b) fin[b] += (uint32_t)__builtin_popcountll(__ballot(fb == b));
   }
@@ -297,7 +285,7 @@ __global__ __launch_bounds__(64) void k_cls_scatter(
     const noise_gpu_record *__restrict__ recs, uint64_t nrec, uint32_t chunk,
     const uint8_t *keys, uint32_t nkeys, const uint8_t *in, const uint8_t *out,
     const unsigned long long *wbase, RecHdr *hdr, uint32_t *idx, SegRec *rt,
-    SegEntry *segs, uint32_t *tails, uint32_t *fin, uint32_t *finl, uint64_t segcap) {
+    SegEntry *segs, uint32_t *tails, uint32_t *fin, uint64_t segcap) {
   const uint32_t lane = threadIdx.x;
   const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
   const uint64_t e0 = b0 + chunk < nrec ? b0 + chunk : nrec;
@@ -354,17 +342,14 @@ __global__ __launch_bounds__(64) void k_cls_scatter(
       run[c] += (unsigned long long)__builtin_popcountll(m);
     }
     {  // long records in finalize order: by segment-count bucket
-      const int fb = cls == kClsLong ? fin_bucket(d.len) : -1;
+      const int fb = cls == kClsLong ? fin_bucket(nf) : -1;
 #pragma unroll
       for (int b = 0; b < kFinBuckets; ++b) {
         const uint64_t m = __ballot(fb == b);
-        if (fb == b) {
-          const unsigned long long pos =
-              fbase[b] + run[kColFin0 + b] +
-              __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-          fin[pos] = (uint32_t)q;
-          finl[pos] = d.len;  // the unit kernel's first load: record and length together
-        }
+        if (fb == b)
+          fin[fbase[b] + run[kColFin0 + b] +
+              __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+              (uint32_t)q;
         run[kColFin0 + b] += (unsigned long long)__builtin_popcountll(m);
       }
     }
@@ -970,8 +955,7 @@ template <bool DECRYPT>
 static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr *hdr,
                                  const uint8_t *keys, uint32_t nkeys,
                                  const noise_gpu_record *recs, const uint32_t *idx,
-                                 const uint32_t *tails, const uint32_t *fin, const uint32_t *finl,
-                                 uint64_t segbound,
+                                 const uint32_t *tails, const uint32_t *fin, uint64_t segbound,
                                  const uint8_t *in,
                                  uint8_t *out, const uint8_t *ad, uint8_t *status,
                                  hipStream_t stream, int chunks) {
@@ -1007,24 +991,6 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
 #define NOISE_DESC_TILE(C, LEN)                                                \
   a.cls = C;                                                                   \
   hipLaunchKernelGGL((k_aead_tile<DECRYPT, LEN, false, kTileDesc>), grid, bt, 0, ax.aux, a);
-  if (DECRYPT && kDecUnits) {
-    // decrypt, long records as units (unit_kernel.hpp): companion: the small
-    // tile classes and the generic kernel; caller: the unit kernel after prep
-    NOISE_DESC_TILES()
-    if ((e = hipEventRecord(ax.join, ax.aux)) != hipSuccess) return e;
-    UnitArgs ua;
-    ua.in = in;
-    ua.out = out;
-    ua.status = status;
-    ua.rt = ta.rt;
-    ua.fin = fin;
-    ua.finl = finl;
-    ua.bucket_cnt = hdr->counts + kColFin0;
-    ua.nlong = &hdr->nlong;
-    hipLaunchKernelGGL(k_unit_dec, dim3(capped(nrec, NOISE_UNIT_GRID)), bt, 0, stream, ua);
-    if ((e = hipStreamWaitEvent(stream, ax.join, 0)) != hipSuccess) return e;
-    return hipGetLastError();
-  }
   if (!DECRYPT) {
     // companion: dense tile classes first, the long-latency tails last (they
     // then overlap the segment kernel's drain; tails first: -3..5 %)
@@ -1113,15 +1079,14 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   const uint64_t segcap = nrec * 63 < kSegCapMax ? nrec * 63 : kSegCapMax;
 
   // scratch: header | part[nw][kCols] | wbase[nw][kCols] | idx[nrec] |
-  //          tails[nrec] | fin[nrec] | finl[nrec] | rt[nrec] | segs[segcap] | partial[segcap] |
+  //          tails[nrec] | fin[nrec] | rt[nrec] | segs[segcap] | partial[segcap] |
   //          partial_hi[segcap]
   const uint64_t o_part = sizeof(RecHdr);
   const uint64_t o_wbase = align_up(o_part + nw * kCols * 4, 256);
   const uint64_t o_idx = align_up(o_wbase + nw * kCols * 8, 256);
   const uint64_t o_tails = align_up(o_idx + nrec * 4, 256);
   const uint64_t o_fin = align_up(o_tails + nrec * 4, 256);
-  const uint64_t o_finl = align_up(o_fin + nrec * 4, 256);
-  const uint64_t o_rt = align_up(o_finl + nrec * 4, 256);
+  const uint64_t o_rt = align_up(o_fin + nrec * 4, 256);
   const uint64_t o_segs = align_up(o_rt + nrec * sizeof(SegRec), 256);
   const uint64_t o_part2 = align_up(o_segs + segcap * sizeof(SegEntry), 256);
   const uint64_t o_phi = align_up(o_part2 + segcap * sizeof(SegPartial), 256);
@@ -1136,7 +1101,6 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   uint32_t *idx = reinterpret_cast<uint32_t *>(base + o_idx);
   uint32_t *tails = reinterpret_cast<uint32_t *>(base + o_tails);
   uint32_t *fin = reinterpret_cast<uint32_t *>(base + o_fin);
-  uint32_t *finl = reinterpret_cast<uint32_t *>(base + o_finl);
   SegRec *rt = reinterpret_cast<SegRec *>(base + o_rt);
   SegEntry *segs = reinterpret_cast<SegEntry *>(base + o_segs);
   SegPartial *partial = reinterpret_cast<SegPartial *>(base + o_part2);
@@ -1145,7 +1109,7 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   const dim3 b64(64);
   hipLaunchKernelGGL(k_cls_count, dim3((unsigned)nw), b64, 0, stream, recs, nrec, (uint32_t)chunk, keys, nkeys, in, out, part);
   hipLaunchKernelGGL(k_cls_scan, dim3(kCols), b64, 0, stream, part, (uint32_t)nw, wbase, hdr, segcap);
-  hipLaunchKernelGGL(k_cls_scatter, dim3((unsigned)nw), b64, 0, stream, recs, nrec, (uint32_t)chunk, keys, nkeys, in, out, wbase, hdr, idx, rt, segs, tails, fin, finl, segcap);
+  hipLaunchKernelGGL(k_cls_scatter, dim3((unsigned)nw), b64, 0, stream, recs, nrec, (uint32_t)chunk, keys, nkeys, in, out, wbase, hdr, idx, rt, segs, tails, fin, segcap);
 
   TileArgs ta{};
   ta.in = in;
@@ -1165,9 +1129,9 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
   // the decrypt pipeline's chunks pay off on large batches only (each chunk
   // adds four launches and a stream hand-off)
   const int chunks = nrec >= kChunkMinRecords ? kSegChunks : 1;
-  return decrypt ? launch_classes<true>(ta, nrec, hdr, keys, nkeys, recs, idx, tails, fin, finl, segcap,
+  return decrypt ? launch_classes<true>(ta, nrec, hdr, keys, nkeys, recs, idx, tails, fin, segcap,
                                        in, out, ad, status, stream, chunks)
-                 : launch_classes<false>(ta, nrec, hdr, keys, nkeys, recs, idx, tails, fin, finl, segcap,
+                 : launch_classes<false>(ta, nrec, hdr, keys, nkeys, recs, idx, tails, fin, segcap,
                                          in, out, ad, status, stream, 1);
 }
 

@@ -40,7 +40,7 @@
 namespace noise_amd {
 
 constexpr int kGenBlock = 256;
-constexpr int kNumTileCls = 6;            // 64 128 192 256 512 1024
+constexpr int kNumTileCls = 10;           // 64 128 192 256 512 1024 2048 4096 8192 16384
 constexpr int kClsLong = kNumTileCls;     // segmented long records
 constexpr int kClsGeneric = kNumTileCls + 1;
 constexpr int kNumCls = kNumTileCls + 2;
@@ -59,7 +59,7 @@ constexpr int kCols = kNumCls + 2 + kFinBuckets;
 #endif
 constexpr int kSegChunks = NOISE_SEG_CHUNKS;
 #ifndef NOISE_CHUNK_W
-#define NOISE_CHUNK_W 2
+#define NOISE_CHUNK_W 4
 #endif
 constexpr unsigned long long kChunkW = NOISE_CHUNK_W;  // chunk c >= 1 : chunk 0
 #ifndef NOISE_CHUNK_MIN  // overridable for the CPU emulation build
@@ -139,6 +139,14 @@ __device__ __forceinline__ int record_class(const noise_gpu_record &d, const uin
     case 256: return 3;
     case 512: return 4;
     case 1024: return 5;  // exactly 1 KiB: one tile-kernel pass beats prep + segment + finalize
+    // whole-record tiles up to 16 KiB (one 16 KiB LDS tile per record at
+    // 16 KiB): the tag is computed and checked in the wave that holds the
+    // record, so decrypt reads it once -- the segment path's verify-first
+    // decrypt reads a long record's ciphertext twice (§4.3 of DESIGN.md)
+    case 2048: return 6;
+    case 4096: return 7;
+    case 8192: return 8;
+    case 16384: return 9;
     default: break;
   }
   return (d.len >= 1024u && d.len <= kLongMax) ? kClsLong : kClsGeneric;
@@ -853,11 +861,13 @@ static inline unsigned capped(uint64_t want, uint64_t cap) {
 struct AuxStream {
   hipStream_t aux = nullptr;   // companion: small classes, generic, tails
   hipStream_t aux2 = nullptr;  // decrypt: per chunk, tag check + plaintext pass
+  hipStream_t aux3 = nullptr;  // the whole-record classes of 2 .. 16 KiB
   // fork: classifier done; prep: k_seg_prep done; join: encrypt: the
   // companion branch done, decrypt: the tails' Poly1305 done; join2: the
   // companion done (decrypt); xdone: the last plaintext pass done; poly[c] /
   // fin[c]: chunk c's Poly1305 pass / tag check done
-  hipEvent_t fork = nullptr, prep = nullptr, join = nullptr, join2 = nullptr, xdone = nullptr;
+  hipEvent_t fork = nullptr, prep = nullptr, join = nullptr, join2 = nullptr, xdone = nullptr,
+             big = nullptr;  // big: the whole-record classes done
   hipEvent_t poly[kSegChunks] = {}, fin[kSegChunks] = {};
 };
 struct AuxEntry {
@@ -883,7 +893,8 @@ static hipError_t aux_get(AuxStream *out, hipStream_t stream) {
   AuxStream a;
   if ((e = hipStreamCreateWithFlags(&a.aux, hipStreamNonBlocking)) != hipSuccess) return e;
   if ((e = hipStreamCreateWithFlags(&a.aux2, hipStreamNonBlocking)) != hipSuccess) return e;
-  for (hipEvent_t *ev : {&a.fork, &a.join, &a.prep, &a.join2, &a.xdone})
+  if ((e = hipStreamCreateWithFlags(&a.aux3, hipStreamNonBlocking)) != hipSuccess) return e;
+  for (hipEvent_t *ev : {&a.fork, &a.join, &a.prep, &a.join2, &a.xdone, &a.big})
     if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return e;
   for (int c = 0; c < kSegChunks; ++c)
     for (hipEvent_t *ev : {&a.poly[c], &a.fin[c]})
@@ -908,13 +919,13 @@ static hipError_t aux_release(int dev, hipStream_t stream) {
   }
   if (!found) return hipSuccess;
   hipError_t e = hipSuccess, e2;
-  for (hipStream_t st : {a.aux, a.aux2}) {
+  for (hipStream_t st : {a.aux, a.aux2, a.aux3}) {
     e2 = hipStreamSynchronize(st);
     if (e == hipSuccess) e = e2;
     e2 = hipStreamDestroy(st);
     if (e == hipSuccess) e = e2;
   }
-  for (hipEvent_t ev : {a.fork, a.prep, a.join, a.join2, a.xdone}) {
+  for (hipEvent_t ev : {a.fork, a.prep, a.join, a.join2, a.xdone, a.big}) {
     e2 = hipEventDestroy(ev);
     if (e == hipSuccess) e = e2;
   }
@@ -979,18 +990,31 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   const dim3 gxor(capped((segbound + 63) / 64, NOISE_GRID_CAP));
   const dim3 gfin(capped((nrec + 64 / NOISE_FIN_W - 1) / (64 / NOISE_FIN_W), NOISE_GRID_CAP));
   RecHdr *hdr_w = const_cast<RecHdr *>(hdr);
+#define NOISE_DESC_BIG(ST)                                                     \
+  NOISE_DESC_TILE(9, 16384, ST)                                                \
+  NOISE_DESC_TILE(8, 8192, ST)                                                 \
+  NOISE_DESC_TILE(7, 4096, ST)                                                 \
+  NOISE_DESC_TILE(6, 2048, ST)
 #define NOISE_DESC_TILES()                                                     \
-  NOISE_DESC_TILE(0, 64)                                                       \
-  NOISE_DESC_TILE(1, 128)                                                      \
-  NOISE_DESC_TILE(2, 192)                                                      \
-  NOISE_DESC_TILE(3, 256)                                                      \
-  NOISE_DESC_TILE(4, 512)                                                      \
-  NOISE_DESC_TILE(5, 1024)                                                     \
+  NOISE_DESC_TILE(0, 64, ax.aux)                                               \
+  NOISE_DESC_TILE(1, 128, ax.aux)                                              \
+  NOISE_DESC_TILE(2, 192, ax.aux)                                              \
+  NOISE_DESC_TILE(3, 256, ax.aux)                                              \
+  NOISE_DESC_TILE(4, 512, ax.aux)                                              \
+  NOISE_DESC_TILE(5, 1024, ax.aux)                                             \
   hipLaunchKernelGGL((k_aead_records<DECRYPT>), gg, dim3(kGenBlock), 0, ax.aux, keys, nkeys, recs,  \
                      nrec, idx, hdr, in, out, ad, status);
-#define NOISE_DESC_TILE(C, LEN)                                                \
+#define NOISE_DESC_TILE(C, LEN, ST)                                            \
   a.cls = C;                                                                   \
-  hipLaunchKernelGGL((k_aead_tile<DECRYPT, LEN, false, kTileDesc>), grid, bt, 0, ax.aux, a);
+  hipLaunchKernelGGL((k_aead_tile<DECRYPT, LEN, false, kTileDesc>), grid, bt, 0, ST, a);
+  // the whole-record classes (2 .. 16 KiB) on a companion of their own, from
+  // the fork: they are a quarter of config 4's bytes and would otherwise
+  // queue behind (or ahead of) the small classes and the tails
+  // (round 5: ahead of encrypt's segment kernel on the caller's stream
+  // instead, encrypt took 5 % longer)
+  if ((e = hipStreamWaitEvent(ax.aux3, ax.fork, 0)) != hipSuccess) return e;
+  NOISE_DESC_BIG(ax.aux3)
+  if ((e = hipEventRecord(ax.big, ax.aux3)) != hipSuccess) return e;
   if (!DECRYPT) {
     // companion: dense tile classes first, the long-latency tails last (they
     // then overlap the segment kernel's drain; tails first: -3..5 %)
@@ -1003,6 +1027,7 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
     if ((e = hipStreamWaitEvent(stream, ax.join, 0)) != hipSuccess) return e;
     hipLaunchKernelGGL((k_seg_finalize_w<DECRYPT, NOISE_FIN_W>), gfin, bt, 0, stream, fin, rt, ta.partial,
                        ta.partial_hi, hdr_w, in, out, status, -1);
+    if ((e = hipStreamWaitEvent(stream, ax.big, 0)) != hipSuccess) return e;
     return hipGetLastError();
   }
   // decrypt.  Companion: the tails' Poly1305 first (the first tag check
@@ -1042,10 +1067,12 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   }
 #undef NOISE_DESC_TILE
 #undef NOISE_DESC_TILES
+#undef NOISE_DESC_BIG
   if ((e = hipEventRecord(ax.xdone, ax.aux2)) != hipSuccess) return e;
   if ((e = hipEventRecord(ax.join2, ax.aux)) != hipSuccess) return e;
   if ((e = hipStreamWaitEvent(stream, ax.xdone, 0)) != hipSuccess) return e;
   if ((e = hipStreamWaitEvent(stream, ax.join2, 0)) != hipSuccess) return e;
+  if ((e = hipStreamWaitEvent(stream, ax.big, 0)) != hipSuccess) return e;
   return hipGetLastError();
 }
 

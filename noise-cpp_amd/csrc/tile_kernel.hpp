@@ -232,17 +232,19 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
           lds_dma16_s<NT>(base, 16u * (r * (C::SPR + 1) + C::SPR), (lds_void *)(lds3 + 64 * q));
       }
     }
-  } else if (MODE >= kTileSeg || (MODE == kTileDesc && C::SPR == 64)) {
-    // 1 KiB units (segments, or kTileDesc records of exactly 1 KiB): DMA
-    // instruction q moves all 64 pieces of unit q, so its offset is
-    // wave-uniform -- read from the unit's key lane (v_readlane into SGPRs)
-    // instead of a per-lane shuffle
+  } else if (MODE >= kTileSeg || (MODE == kTileDesc && C::SPR % 64 == 0)) {
+    // whole KiB (segments, kTileDesc records of 1 KiB .. 16 KiB): DMA
+    // instruction q moves KiB q % (SPR / 64) of unit q / (SPR / 64), so its
+    // offset is wave-uniform -- read from the unit's key lane (v_readlane into
+    // SGPRs) instead of a per-lane shuffle
+    constexpr int KPR = C::SPR / 64;  // KiB per unit
 #pragma unroll
-    for (int q = 0; q < C::RPT; ++q) {
-      if ((uint32_t)q < nv) {
-        const uint32_t kl = t_rpt + q;
+    for (int q = 0; q < C::REC_SLOTS / 64; ++q) {
+      if ((uint32_t)(q / KPR) < nv) {
+        const uint32_t kl = t_rpt + q / KPR;
         const uint64_t off = join64((uint32_t)__builtin_amdgcn_readlane((int)own_in_hi, (int)kl),
-                                    (uint32_t)__builtin_amdgcn_readlane((int)own_in_lo, (int)kl));
+                                    (uint32_t)__builtin_amdgcn_readlane((int)own_in_lo, (int)kl)) +
+                             1024ull * (q % KPR);
         lds_dma16_s<NT>(in + off, 16u * glq<SPAN>(gl, q), (lds_void *)(lds3 + 64 * q));
       }
     }
@@ -400,9 +402,15 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     seg_meta_load<MODE, SPAN>(nxt, a.rt, nxt_e, g < nrec, in, out);
   }
 
+  // records per super-tile: 64 (one key lane each), but at most 128 KiB for
+  // descriptor classes of 4 KiB and up (8 tiles), so that a class of tens of
+  // thousands of 16 KiB records still makes thousands of waves
+  constexpr int RPS = (MODE == kTileDesc && L > 2048) ? 64 * 2048 / L : 64;
+  constexpr int NTS = RPS / C::RPT;  // tiles per super-tile
+  static_assert(RPS == 64 || (!SEG && NTS >= 1 && RPS % C::RPT == 0), "super-tile shape");
 #pragma unroll 1
-  for (uint64_t super0 = (uint64_t)blockIdx.x * 64; super0 < nrec;
-       super0 += (uint64_t)gridDim.x * 64) {
+  for (uint64_t super0 = (uint64_t)blockIdx.x * RPS; super0 < nrec;
+       super0 += (uint64_t)gridDim.x * RPS) {
   // ---- key pass: lane l -> one-time key of record super0 + l -------------
   uint32_t kr[4], kss[4];
   F26 pw[C::LOG2G > 0 && !SEG ? C::LOG2G : 1];  // uniform / keyed: r^BPL, r^(2 BPL), ...
@@ -447,7 +455,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
       const uint64_t rec = super0 + lane;
       uint32_t ki = 0;
       n = 0;
-      if (rec < nrec) {
+      if (rec < nrec && lane < (uint32_t)RPS) {
         if (MODE == kTileSessions) {
           ki = __builtin_nontemporal_load(a.key_idx + rec);
           n = __builtin_nontemporal_load(a.nonces + rec);
@@ -505,7 +513,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
 
   bool prev_all = false;  // the previous tile issued all NOUT of its stores
 #pragma unroll 1
-  for (int t = 0; t < C::G; ++t) {
+  for (int t = 0; t < NTS; ++t) {
     const uint64_t rec0 = super0 + (uint64_t)t * C::RPT;
     if (rec0 >= nrec) break;
     const uint32_t nv = (nrec - rec0) < (uint64_t)C::RPT ? (uint32_t)(nrec - rec0) : C::RPT;
@@ -531,7 +539,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
       own_pw.a[0] = m ? v.x : 1u; own_pw.a[1] = m ? v.y : 0u; own_pw.a[2] = m ? v.z : 0u;
       own_pw.a[3] = m ? v.w : 0u; own_pw.a[4] = m ? v4 : 0u;
     }
-    if (NBUF == 2 && t + 1 < C::G) {  // the next tile's DMA now, into the other buffer
+    if (NBUF == 2 && t + 1 < NTS) {  // the next tile's DMA now, into the other buffer
       const uint64_t nrec0 = rec0 + C::RPT;
       if (nrec0 < nrec) {
         const uint64_t left = nrec - nrec0;
@@ -696,7 +704,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     wave_lds_fence();
     if (!DO_XOR) {  // kTileSegPoly: nothing to store; the next tile's DMA
       prev_all = false;
-      if (t + 1 < C::G) {
+      if (t + 1 < NTS) {
         const uint64_t nrec0 = rec0 + C::RPT;
         if (nrec0 < nrec) {
           wait_lds();  // this tile's LDS reads done before the DMA overwrites them
@@ -719,10 +727,11 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     constexpr int NPART = (KEYED && NBUF == 1 && NOUT > 8) ? 2 : 1;
     constexpr int NQ = (NOUT + NPART - 1) / NPART;
     const bool full = nv == (uint32_t)C::RPT;
-    // RECQ (1 KiB units: segments, 1 KiB descriptor records): output
-    // instruction q < RPT holds the 64 data pieces of record q (uniform
-    // destination, v_readlane), instruction RPT (encrypt) the RPT tags
-    constexpr bool RECQ = SEG || (MODE == kTileDesc && C::SPR == 64);
+    // RECQ (segments, descriptor records of whole KiB): output instruction
+    // q < NDATA holds the 64 data pieces of KiB q % (SPR / 64) of record
+    // q / (SPR / 64) (uniform destination, v_readlane), instruction NDATA
+    // (encrypt) the RPT tags
+    constexpr bool RECQ = SEG || (MODE == kTileDesc && C::SPR % 64 == 0);
     auto piece = [&](int q, uint32_t &r, uint32_t &pc, uint32_t &slot, bool &ok) {
       if constexpr (RECW) {
         if (q < NDATA) {
@@ -739,8 +748,11 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
         return;
       }
       if (RECQ) {
-        if (q < C::RPT) {
-          r = (uint32_t)q; pc = lane; slot = swz<SPAN>(64u * q + lane); ok = true;
+        if (q < NDATA) {
+          r = (uint32_t)q / (C::SPR / 64);
+          pc = 64u * ((uint32_t)q % (C::SPR / 64)) + lane;
+          slot = swz<SPAN>(64u * q + lane);
+          ok = true;
         } else {
           r = lane < (uint32_t)C::RPT ? lane : 0u; pc = C::SPR; slot = C::REC_SLOTS + r;
           ok = lane < (uint32_t)C::RPT;
@@ -794,7 +806,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
         wait_lds();  // LDS reads done
         wave_lds_fence();
         // ---- NBUF = 1: next tile's DMA, then these stores, both in flight
-        if (NBUF == 1 && t + 1 < C::G) {
+        if (NBUF == 1 && t + 1 < NTS) {
           const uint64_t nrec0 = rec0 + C::RPT;
           if (nrec0 < nrec) {
             const uint64_t left = nrec - nrec0;
@@ -816,8 +828,8 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
         bool store = st[qq];
         if (ABL == 1) store = store && (ov[qq].x == 0x12345678u && ov[qq].y == 0x9abcdef0u);
         uint8_t *dst;
-        if (RECQ && q < C::RPT) {  // output instruction q = record / segment q: uniform offset
-          const uint32_t kl = (uint32_t)t * C::RPT + (uint32_t)q;
+        if (RECQ && q < NDATA) {  // output instruction q: a KiB of one record / segment: uniform offset
+          const uint32_t kl = (uint32_t)t * C::RPT + (uint32_t)q / (C::SPR / 64);
           const uint64_t off = join64((uint32_t)__builtin_amdgcn_readlane((int)own_out_hi, (int)kl),
                                       (uint32_t)__builtin_amdgcn_readlane((int)own_out_lo, (int)kl));
           dst = out + off + 16u * pc;

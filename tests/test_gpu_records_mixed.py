@@ -357,3 +357,65 @@ def test_chunked_decrypt_pipeline_tamper(oracle, in_place):
             assert back[o:o + L] == pts[i], (i, L)
         if not in_place:
             assert back[o + L:o + L + 16] == b"\x3c" * 16, ("wrote past the record", i, L)
+
+
+@pytest.mark.parametrize("in_place", [False, True], ids=["copy", "in_place"])
+def test_whole_record_classes_tamper(oracle, in_place):
+    """Records of exactly 2, 4, 8 and 16 KiB take the whole-record tile
+    classes (records_kernels.hip, round 5; 128 KiB super-tiles from 4 KiB up):
+    every tag is checked in the wave that holds the record, before its
+    plaintext is stored (crypto_aead_read, monocypher.c:2912-2929).  2400
+    records (several super-tiles per class and partial last ones), every 7th
+    tampered in a ciphertext or tag byte: bit-exact against the oracle,
+    REC_BAD_MAC, a failed copy zeroed, a failed in-place record untouched,
+    nothing written past a record."""
+    rng = random.Random(4096 + in_place)
+    nkeys = 9
+    keys = [rng.randbytes(32) for _ in range(nkeys)]
+    recs = []
+    for L in (2048, 4096, 8192, 16384):
+        for _ in range(600 - 7 * (L >> 12)):  # class sizes not multiples of a super-tile
+            recs.append([L, b"", rng.randrange(nkeys), rng.getrandbits(64) % (2**64 - 2), 0, 0])
+    rng.shuffle(recs)
+    pts = [rng.randbytes(r[0]) for r in recs]
+    cts = [bytearray(oracle.encrypt(keys[r[2]], r[3], b"", pts[i])) for i, r in enumerate(recs)]
+    bad = set(range(3, len(recs), 7))
+    for i in bad:
+        cts[i][rng.randrange(recs[i][0] + 16)] ^= 1 << rng.randrange(8)
+    d_keys = dev(b"".join(keys))
+    d_st = torch.full((len(recs),), 9, dtype=torch.uint8, device="cuda")
+    if in_place:
+        desc, nbytes, _, _ = layout(recs, decrypt=True, in_place=True)
+        buf = bytearray(nbytes)
+        fill(buf, desc, cts, "in_off")
+        d_buf = dev(buf)
+        noise_amd.decrypt_records(d_keys, nkeys, dev(desc.view(np.uint8)), len(recs), d_buf, d_buf, d_st,
+                                  dev(b""))
+        res = host(d_buf)
+        st = host(d_st)
+        for i, (L, _, _, _, _, _) in enumerate(recs):
+            o = int(desc[i]["in_off"])
+            if i in bad:
+                assert st[i] == noise_amd.REC_BAD_MAC, (i, L)
+                assert res[o:o + L + 16] == bytes(cts[i]), ("in-place failure must keep ct", i, L)
+            else:
+                assert st[i] == noise_amd.REC_OK, (i, L, st[i])
+                assert res[o:o + L] == pts[i], (i, L)
+        return
+    desc, din, dout, _ = layout(recs, decrypt=True)
+    cin = bytearray(din)
+    fill(cin, desc, cts, "in_off")
+    d_back = torch.full((dout,), 0x3C, dtype=torch.uint8, device="cuda")
+    noise_amd.decrypt_records(d_keys, nkeys, dev(desc.view(np.uint8)), len(recs), dev(cin), d_back, d_st,
+                              dev(b""))
+    back = host(d_back)
+    st = host(d_st)
+    for i, (L, _, _, _, _, _) in enumerate(recs):
+        o = int(desc[i]["out_off"])
+        if i in bad:
+            assert st[i] == noise_amd.REC_BAD_MAC, (i, L)
+            assert back[o:o + L] == bytes(L), ("failed copy must be zeroed", i, L)
+        else:
+            assert st[i] == noise_amd.REC_OK, (i, L, st[i])
+            assert back[o:o + L] == pts[i], (i, L)
+        assert back[o + L:o + L + 16] == b"\x3c" * 16, ("wrote past the record", i, L)

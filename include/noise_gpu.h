@@ -123,7 +123,8 @@ int noise_gpu_decrypt_uniform(const uint8_t h_key[32], uint64_t nonce0,
  * Batches of >= 2048 records are load-balanced on the device, stream-ordered
  * (no host synchronisation): records are sorted by class and each class
  * runs its own kernel -- 16-byte aligned AD-free records of 64, 128, 192,
- * 256, 512 and 1024 bytes on the LDS-staged tile kernel; aligned AD-free
+ * 256, 512, 1024, 2048, 4096, 8192 and 16384 bytes on the LDS-staged tile
+ * kernel (a record up to 16 KiB whole in one wave); other aligned AD-free
  * records of 1024..65535 bytes (any length) cut into 1 KiB segments that ONE
  * tile-kernel launch processes, plus a tail kernel and a per-record finalize
  * (tag); everything else one lane per record.  Every path checks a record's

@@ -95,12 +95,6 @@ constexpr int kHdrWords = kSegChunks <= 4 ? 64 : 256;    // scratch header: 512 
 constexpr uint32_t kClsWaves = NOISE_CLS_WAVES;
 constexpr uint64_t kClsMinChunk = NOISE_CLS_MIN_CHUNK;
 static_assert(kClsWaves % 64 == 0 && kClsMinChunk % 64 == 0, "classifier geometry");
-// grid cap of the generic (lane per record) kernel, which strides over its
-// records (BASELINE-like batches have none)
-#ifndef NOISE_GEN_GRID
-#define NOISE_GEN_GRID 4096u
-#endif
-constexpr unsigned kGenGridCap = NOISE_GEN_GRID;
 #ifndef NOISE_CLASSIFY_MIN  // overridable for the CPU emulation build
 #define NOISE_CLASSIFY_MIN 2048
 #endif
@@ -990,7 +984,7 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   if ((e = hipEventRecord(ax.prep, stream)) != hipSuccess) return e;
   TileArgs a = ta;
   const uint64_t gblocks = (nrec + kGenBlock - 1) / kGenBlock;
-  const dim3 gg((unsigned)(gblocks < kGenGridCap ? gblocks : kGenGridCap));
+  const dim3 gg((unsigned)(gblocks < 2 * NOISE_GRID_CAP ? gblocks : 2 * NOISE_GRID_CAP));
   const dim3 gseg(capped((segbound + 63) / 64, NOISE_GRID_CAP));
   const dim3 gpoly(capped((segbound + 63) / 64, NOISE_GRID_CAP));
   const dim3 gxor(capped((segbound + 63) / 64, NOISE_GRID_CAP));

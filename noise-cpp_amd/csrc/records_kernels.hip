@@ -36,16 +36,14 @@
 #include "launchers.hpp"
 #include "noise_amd/dev_mem.hpp"
 #include "tile_kernel.hpp"
-#include "rec32_kernel.hpp"
 
 namespace noise_amd {
 
 constexpr int kGenBlock = 256;
 constexpr int kNumTileCls = 10;           // 64 128 192 256 512 1024 2048 4096 8192 16384
-constexpr int kClsRec32 = kNumTileCls;    // exactly 32 KiB: a wave per record (k_rec32)
-constexpr int kClsLong = kNumTileCls + 1; // segmented long records
-constexpr int kClsGeneric = kNumTileCls + 2;
-constexpr int kNumCls = kNumTileCls + 3;
+constexpr int kClsLong = kNumTileCls;     // segmented long records
+constexpr int kClsGeneric = kNumTileCls + 1;
+constexpr int kNumCls = kNumTileCls + 2;
 constexpr int kColSegs = kNumCls;         // classifier column: full segments
 constexpr int kColTails = kNumCls + 1;    // classifier column: long records with a tail
 constexpr int kColFin0 = kNumCls + 2;     // classifier columns: long records by
@@ -97,12 +95,6 @@ constexpr int kHdrWords = kSegChunks <= 4 ? 64 : 256;    // scratch header: 512 
 constexpr uint32_t kClsWaves = NOISE_CLS_WAVES;
 constexpr uint64_t kClsMinChunk = NOISE_CLS_MIN_CHUNK;
 static_assert(kClsWaves % 64 == 0 && kClsMinChunk % 64 == 0, "classifier geometry");
-// records of exactly 32 KiB: 1 = one wave per record, resident in LDS
-// (k_rec32, rec32_kernel.hpp), 0 = segments
-#ifndef NOISE_REC32
-#define NOISE_REC32 1
-#endif
-constexpr bool kRec32 = NOISE_REC32 != 0;
 #ifndef NOISE_CLASSIFY_MIN  // overridable for the CPU emulation build
 #define NOISE_CLASSIFY_MIN 2048
 #endif
@@ -155,7 +147,6 @@ __device__ __forceinline__ int record_class(const noise_gpu_record &d, const uin
     case 4096: return 7;
     case 8192: return 8;
     case 16384: return 9;
-    case 32768: return kRec32 ? kClsRec32 : kClsLong;
     default: break;
   }
   return (d.len >= 1024u && d.len <= kLongMax) ? kClsLong : kClsGeneric;
@@ -1022,11 +1013,6 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   // (round 5: ahead of encrypt's segment kernel on the caller's stream
   // instead, encrypt took 5 % longer)
   if ((e = hipStreamWaitEvent(ax.aux3, ax.fork, 0)) != hipSuccess) return e;
-  if (kRec32) {
-    a.cls = kClsRec32;
-    hipLaunchKernelGGL((k_rec32<DECRYPT>), dim3(capped((nrec + kRec32RPS - 1) / kRec32RPS, NOISE_GRID_CAP)),
-                       bt, 0, ax.aux3, a);
-  }
   NOISE_DESC_BIG(ax.aux3)
   if ((e = hipEventRecord(ax.big, ax.aux3)) != hipSuccess) return e;
   if (!DECRYPT) {

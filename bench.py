@@ -95,9 +95,13 @@ def reduce_over_ranks(dist, elapsed, nrec, device):
 
 
 def device_info(args, local):
-    """The rank's device: index, name and PCI bus id (the stub: the host)."""
+    """The rank's device: index, name and PCI bus id (the stub: the host, with
+    a made-up PCI address per rank -- or one shared by all ranks with the
+    test hook --stub-same-device -- so that the aliasing check runs)."""
     if args.stub:
-        return {"index": None, "name": "cpu (stub)"}
+        bus = 0 if args.stub_same_device else int(os.environ.get("RANK", "0"))
+        return {"index": None, "name": "cpu (stub)", "pci_domain_id": 0, "pci_bus_id": bus,
+                "pci_device_id": 0}
     import torch
     p = torch.cuda.get_device_properties(local)
     info = {"index": local, "name": p.name}
@@ -107,13 +111,44 @@ def device_info(args, local):
     return info
 
 
-def check_shards(shards):
-    """Rank shard table -> error text if two ranks share a nonce."""
+def device_key(dev):
+    """A device's identity across processes: its PCI address, or None when the
+    runtime does not report one."""
+    if not dev or dev.get("pci_bus_id") is None:
+        return None
+    return (dev.get("pci_domain_id", 0), dev["pci_bus_id"], dev.get("pci_device_id", 0))
+
+
+def check_shards(shards, share_device=False):
+    """Rank shard table -> error text if two ranks share a nonce, or -- unless
+    the ranks were told to share the visible GPUs (--share-device, a test
+    hook) -- two ranks ran on one device: an N-rank line whose ranks doubled
+    up on a card (a LOCAL_RANK or visibility mishap) is not an N-GPU figure."""
     spans = sorted((s["nonce_lo"], s["nonce_hi"], s["rank"]) for s in shards)
     for a, b in zip(spans, spans[1:]):
         if b[0] < a[1]:
             return "ranks %d and %d share nonces [%d, %d)" % (a[2], b[2], b[0], min(a[1], b[1]))
+    if not share_device:
+        seen = {}
+        for s in sorted(shards, key=lambda x: x["rank"]):
+            k = device_key(s.get("device"))
+            if k is None:
+                continue
+            if k in seen:
+                return "ranks %d and %d ran on the same device (PCI %04x:%02x:%02x); an N-GPU line needs " \
+                       "one device per rank" % (seen[k], s["rank"], k[0], k[1], k[2])
+            seen[k] = s["rank"]
     return None
+
+
+def rank_spread(shards):
+    """max / min over ranks of each rank's own per-launch times (1.0 = even)."""
+    out = {}
+    for f in ("enc_ms", "dec_ms", "step_ms"):
+        v = [s[f] for s in shards if s.get(f)]
+        if v:
+            out[f] = {"min": min(v), "max": max(v), "max_over_min": round(max(v) / min(v), 4)}
+    return out
 
 
 # ---------------------------------------------------------------- launcher
@@ -204,7 +239,7 @@ def pmc_kernels(prof, names, anchor=None):
 
 
 # ---------------------------------------------------------------- cpu leg
-def cpu_sample(cfg, orc, nbytes):
+def cpu_sample(cfg, orc, nbytes, jitter=False):
     """A bounded sample of config `cfg`'s own records (same seeds, shapes and
     nonces as make_workload, rank 0), about `nbytes` of plaintext, as a
     descriptor batch: (key table, descriptors, plaintext, ct buffer size,
@@ -230,15 +265,15 @@ def cpu_sample(cfg, orc, nbytes):
         what = ("the first %d records of the 65536-session x 16 batch (record i: session i mod "
                 "65536, nonce (s << 32) + i div 65536), 1 KiB" % R)
     elif cfg == 4:
-        allr = zipf_lengths(1 << 20)
+        allr = zipf_lengths(1 << 20, jitter)
         csum = np.cumsum(allr)
         R = int(max(64, np.searchsorted(csum, nbytes)))
         lens = allr[:R]
         keys = np.frombuffer(KEY, dtype=np.uint8).copy()
         kidx = np.zeros(R, dtype=np.uint32)
         nonce = np.arange(R, dtype=np.uint64)
-        what = ("the first %d records of the Zipf batch (64 B .. 65519 B, mean %d B), one key"
-                % (R, int(lens.sum() // R)))
+        what = ("the first %d records of the %sZipf batch (64 B .. 65519 B, mean %d B), one key"
+                % (R, "jittered " if jitter else "", int(lens.sum() // R)))
     else:
         raise ValueError(cfg)
     in_sz = (lens + np.uint64(15)) // np.uint64(16) * np.uint64(16)
@@ -251,7 +286,7 @@ def cpu_sample(cfg, orc, nbytes):
     return keys, d, pt, int(ct_sz.sum()), int(lens.sum()), what
 
 
-def cpu_baseline(cfg=2):
+def cpu_baseline(cfg=2, jitter=False):
     """The reference's own monocypher.c (oracle/_ref: the reference source
     built by oracle/Makefile, with the noise::encrypt / decrypt nonce framing
     of noise.cpp:202-281) -- or the build's C restatement if _ref is absent --
@@ -267,7 +302,7 @@ def cpu_baseline(cfg=2):
     orc = oracle_lib.Oracle()
     ncpu = os.cpu_count() or 1
     share = min(SHARE_CPUS, ncpu)
-    keys, desc, pt, ct_bytes, pt_bytes, what = cpu_sample(cfg, orc, 256 << 20)
+    keys, desc, pt, ct_bytes, pt_bytes, what = cpu_sample(cfg, orc, 256 << 20, jitter)
     R = len(desc)
     ct = np.zeros(ct_bytes, dtype=np.uint8)
     back = np.zeros(len(pt), dtype=np.uint8)
@@ -392,16 +427,26 @@ def mix64_np(z):
     return z ^ (z >> np.uint64(31))
 
 
-def zipf_lengths(R):
+JITTER_SEED = 0x4A4954  # "JIT"
+
+
+def zipf_lengths(R, jitter=False):
     """Config 4 record lengths: 64 * 2^k, P(k) ~ 1/(k+1), k = 0..10 drawn by
-    inverse CDF from splitmix64(seed 4); the top bucket clamped to 65519."""
+    inverse CDF from splitmix64(seed 4); the top bucket clamped to 65519.
+    jitter: the same buckets, each length lowered by
+    U(0..63) (splitmix64(seed 0x4A4954) mod 64), so that almost no record has
+    a power-of-two size: 64 * 2^k - U, clamped to 1 .. 65519."""
     import numpy as np
     w = np.array([1.0 / (k + 1) for k in range(11)])
     cdf = np.cumsum(w / w.sum())
-    u = mix64_np(np.uint64(4) + (np.arange(R, dtype=np.uint64) + np.uint64(1)) *
-                 np.uint64(0x9e3779b97f4a7c15)).astype(np.float64) / 2.0 ** 64
+    i1 = np.arange(R, dtype=np.uint64) + np.uint64(1)
+    u = mix64_np(np.uint64(4) + i1 * np.uint64(0x9e3779b97f4a7c15)).astype(np.float64) / 2.0 ** 64
     k = np.minimum(np.searchsorted(cdf, u, side="right"), 10)
-    return np.minimum(64 << k, 65519).astype(np.uint64)
+    lens = (64 << k).astype(np.int64)
+    if jitter:
+        lens -= (mix64_np(np.uint64(JITTER_SEED) + i1 * np.uint64(0x9e3779b97f4a7c15)) %
+                 np.uint64(64)).astype(np.int64)
+    return np.clip(lens, 1, 65519).astype(np.uint64)
 
 
 def tile_symbol(dec, L, contig, mode):
@@ -520,7 +565,7 @@ def make_workload(cfg, args, rank, world, stream):
                   "pt": d_pt, "ct": d_ct, "back": d_back, "status": d_st}
     elif cfg == 4:
         R = args.records or (1 << 20)
-        lens = zipf_lengths(R)
+        lens = zipf_lengths(R, args.jitter)
         # records packed at 16-byte alignment (--rec-align: a layout study)
         al = np.uint64(args.rec_align)
         in_sz = (lens + al - np.uint64(1)) // al * al
@@ -555,8 +600,13 @@ def make_workload(cfg, args, rank, world, stream):
             if evs:
                 evs[2].record(stream)
         workload = "cfg4: 2^20 records per GPU, 64 B .. 65519 B (P(k) ~ 1/(k+1)), one key"
+        if args.jitter:
+            workload = ("cfg4-jitter: 2^20 records per GPU, 64 * 2^k - U(0..63) B (P(k) ~ 1/(k+1)), "
+                        "clamped to 1 .. 65519, one key")
         metric = "GiB/s ChaChaPoly AEAD over device-resident mixed-size Noise records"
-        cfgd = {"mean_record_bytes": L, "total_plaintext_bytes": int(lens.sum()), "keys": 1}
+        cfgd = {"mean_record_bytes": L, "total_plaintext_bytes": int(lens.sum()), "keys": 1,
+                "jitter": bool(args.jitter), "record_align": int(args.rec_align),
+                "records_pow2_len": int(np.count_nonzero((lens & (lens - np.uint64(1))) == 0))}
         pt_bytes = int(lens.sum())
         lens_t = torch.from_numpy(lens.astype(np.int64)).cuda()
         off_t = torch.from_numpy(in_off.astype(np.int64)).cuda()
@@ -663,10 +713,16 @@ def parse(argv):
     ap.add_argument("--check-oracle", action="store_true", help=argparse.SUPPRESS)
     # layout study (config 4): byte alignment of each record's offsets
     ap.add_argument("--rec-align", type=int, default=16, help=argparse.SUPPRESS)
+    # config 4 with ragged lengths: 64 * 2^k - U(0..63) (zipf_lengths)
+    ap.add_argument("--jitter", action="store_true",
+                    help="config 4: lower each record length by U(0..63) bytes")
     # test hook: ranks share the visible GPUs (rank r -> device r mod count),
     # so the N-rank path runs end to end on a 1-GPU box (the rate is then
     # not a scaling figure: the ranks split one GPU)
     ap.add_argument("--share-device", action="store_true", help=argparse.SUPPRESS)
+    # test hook (--stub only): every rank reports the same device, which the
+    # shard check must refuse unless --share-device is given
+    ap.add_argument("--stub-same-device", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
 
@@ -781,7 +837,11 @@ def main(argv=None):
         shards = gathered
     else:
         total_rec = R
-    bad = check_shards(shards) if cfg != 3 else None
+    if cfg == 3:  # sessions: nonces are per session, so only the devices are compared
+        bad = check_shards([dict(s, nonce_lo=s["rank"], nonce_hi=s["rank"] + 1) for s in shards],
+                           args.share_device)
+    else:
+        bad = check_shards(shards, args.share_device)
     if bad:
         raise SystemExit("shard table: " + bad)
     log("enc %.3f ms, dec %.3f ms per launch; step %.3f ms" %
@@ -801,17 +861,19 @@ def main(argv=None):
                             "parallelism": "records sharded per GPU, no collective"},
                            **wl["config"]),
             "roofline": roofline(cfg, wl, enc_ms, dec_ms),
-            "shards": shards}
+            "shards": shards, "rank_spread": rank_spread(shards)}
     if args.share_device:
         line["note"] = "--share-device test run: the ranks split the visible GPU(s); not a scaling figure"
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.stub:
         log("cpu baseline ...")
-        line["cpu_baseline"] = cpu_baseline(cfg)
+        line["cpu_baseline"] = cpu_baseline(cfg, args.jitter)
     if rank == 0 and world == 1 and cfg == 2 and not args.no_config1 and not args.stub:
         log("config 1 leg ...")
         line["config1"] = config1()
     if rank == 0 and args.host_inclusive and cfg == 2 and not args.stub:
-        line["host_inclusive"] = host_inclusive(R, L)
+        # 1 KiB (the config-2 shape) and 16 KiB records, the same 1 GiB each
+        line["host_inclusive"] = dict(host_inclusive(R, L), record_bytes=L)
+        line["host_inclusive_16k"] = dict(host_inclusive(R * L // 16384, 16384), record_bytes=16384)
     if rank == 0:
         out.write(json.dumps(line) + "\n")
         out.flush()

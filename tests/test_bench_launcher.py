@@ -128,3 +128,37 @@ def test_roofline_fields_from_committed_profiles(cfg):
         cap = roof["valu_cap_hbm_frac"]
         assert roof["hbm_frac_rw"] < cap < 1.0
         assert abs(roof["hbm_frac_rw"] / cap - v["frac"]) < 0.01
+
+
+def test_two_ranks_on_one_device_refused():
+    """an N-rank line whose ranks report the same
+    device (PCI address) is refused -- non-zero exit, no JSON line -- unless
+    the ranks were told to share the GPU (--share-device, the 1-GPU-box test
+    hook), in which case the line is printed and says so."""
+    p = run_bench("--records", "64", "--stub-same-device", gpus=2)
+    assert p.returncode != 0
+    assert "same device" in p.stderr
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    p = run_bench("--records", "64", "--stub-same-device", "--share-device", gpus=2)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["n_gpus"] == 2 and "share-device" in d["note"]
+    # the per-rank spread of the launch times is in the line
+    for f in ("enc_ms", "dec_ms", "step_ms"):
+        sp = d["rank_spread"][f]
+        assert sp["max"] >= sp["min"] > 0 and sp["max_over_min"] >= 1.0
+
+
+def test_check_shards_device_aliasing():
+    sys.path.insert(0, ROOT)
+    import bench
+    dev = lambda bus: {"index": 0, "name": "x", "pci_domain_id": 0, "pci_bus_id": bus, "pci_device_id": 0}
+    two = [{"rank": 0, "nonce_lo": 0, "nonce_hi": 10, "device": dev(5)},
+           {"rank": 1, "nonce_lo": 10, "nonce_hi": 20, "device": dev(5)}]
+    assert "same device" in bench.check_shards(two)
+    assert bench.check_shards(two, share_device=True) is None
+    two[1]["device"] = dev(6)
+    assert bench.check_shards(two) is None
+    # no PCI address reported: nothing to compare
+    two[0]["device"] = two[1]["device"] = {"index": 0, "name": "x"}
+    assert bench.check_shards(two) is None

@@ -38,6 +38,32 @@ std::uint64_t records_before_limit(std::uint64_t n, std::uint64_t count) {
 
 }  // namespace
 
+void encrypt(std::array<std::uint8_t, 32> &k, std::uint64_t n,
+             std::optional<std::vector<std::uint8_t>> ad,
+             std::vector<std::uint8_t> &in_out) {
+  const std::size_t text_size = in_out.size();
+  in_out.resize(text_size + 16);
+  const int rc = noise_gpu_encrypt_host(k.data(), n, ad ? ad->data() : nullptr, ad ? ad->size() : 0,
+                                        in_out.data(), text_size);
+  wipe(k.data(), k.size());  // noise.cpp:222
+  if (rc != NOISE_GPU_OK) {
+    in_out.resize(text_size);
+    throw_status(rc);
+  }
+}
+
+void decrypt(std::array<std::uint8_t, 32> &k, std::uint64_t n,
+             std::optional<std::vector<std::uint8_t>> ad,
+             std::vector<std::uint8_t> &in_out) {
+  const int rc = in_out.size() < 16
+                     ? NOISE_GPU_E_MAC
+                     : noise_gpu_decrypt_host(k.data(), n, ad ? ad->data() : nullptr, ad ? ad->size() : 0,
+                                              in_out.data(), in_out.size());
+  wipe(k.data(), k.size());  // noise.cpp:272-273 / 278
+  if (rc != NOISE_GPU_OK) throw_status(rc);
+  in_out.resize(in_out.size() - 16);
+}
+
 CipherState::~CipherState() {
   wipe(k.data(), k.size());
   n = std::numeric_limits<std::uint64_t>::max();

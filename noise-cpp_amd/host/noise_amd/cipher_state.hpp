@@ -26,6 +26,7 @@
 #include <concepts>
 #include <cstddef>
 #include <cstdint>
+#include <optional>
 #include <stdexcept>
 #include <vector>
 
@@ -40,6 +41,28 @@ concept STLContainer = requires(T container) {
   { container.size() } -> std::same_as<std::size_t>;
 };
 #endif
+
+// The reference's exported free functions (noise.cpp:202-224 encrypt,
+// 254-281 decrypt; `T` symbols of its library, declared nowhere public), with
+// the same signature -- so the same mangled name -- on the GPU engine:
+//   encrypt: in_out grows by 16 (ct || tag, noise.cpp:206) under the nonce
+//            0^32 || LE64(n) (noise.cpp:207-215), AD = *ad when present;
+//   decrypt: the tag is checked first; on failure in_out is left untouched
+//            and std::invalid_argument("Invalid MAC") is thrown (noise.cpp:
+//            269-276), else it shrinks by 16 (noise.cpp:280);
+//   both wipe the caller's key k after use, as the reference does
+//            (crypto_wipe(k), noise.cpp:221-223 / 277-279).
+// Deviations, as for CipherState: decrypt of fewer than 16 bytes throws
+// invalid_argument("Invalid MAC") (the reference underflows, noise.cpp:257);
+// an all-zero k is "no key" (noise_gpu.h) and throws invalid_argument;
+// no gfx950 device -> std::runtime_error.  No nonce-limit check here: that
+// rule is CipherState's (noise.cpp:398), the free functions have none.
+void encrypt(std::array<std::uint8_t, 32> &k, std::uint64_t n,
+             std::optional<std::vector<std::uint8_t>> ad,
+             std::vector<std::uint8_t> &in_out);
+void decrypt(std::array<std::uint8_t, 32> &k, std::uint64_t n,
+             std::optional<std::vector<std::uint8_t>> ad,
+             std::vector<std::uint8_t> &in_out);
 
 class CipherState {
 private:

@@ -13,6 +13,7 @@
 #include <cstring>
 #include <fstream>
 #include <limits>
+#include <optional>
 #include <sstream>
 #include <stdexcept>
 #include <string>
@@ -43,6 +44,11 @@ static std::array<std::uint8_t, 32> key32(const std::string &h) {
   Bytes b = unhex(h);
   std::memcpy(k.data(), b.data(), 32);
   return k;
+}
+static bool zero32(const std::array<std::uint8_t, 32> &k) {
+  for (auto b : k)
+    if (b) return false;
+  return true;
 }
 static std::vector<std::vector<std::string>> read_tsv(const std::string &path) {
   std::vector<std::vector<std::string>> rows;
@@ -227,6 +233,52 @@ static void gpu_checks(const std::string &dir) {
     CHECK(threw && four[0].size() == 17 && four[1].size() == 17 && four[2].size() == 1,
           "batch stops at the nonce limit after 2 records");
     CHECK(lim.nonce() == std::numeric_limits<std::uint64_t>::max() - 1, "n at the limit");
+  }
+  // 7. the reference's free functions noise::encrypt / noise::decrypt
+  // (noise.cpp:202-224, 254-281) over every golden record: same bytes, the
+  // caller's key wiped after each call, resize +-16, Invalid MAC on a tamper
+  // with the buffer untouched
+  {
+    int nf = 0;
+    for (auto &r : tr) {
+      auto k = key32(r[2]);
+      Bytes m = unhex(r[4]);
+      noise::encrypt(k, std::stoull(r[3]), std::nullopt, m);
+      CHECK(m == unhex(r[5]), "free encrypt %s n=%s", r[0].c_str(), r[3].c_str());
+      CHECK(zero32(k), "free encrypt must wipe the key (noise.cpp:222)");
+      k = key32(r[2]);
+      noise::decrypt(k, std::stoull(r[3]), std::nullopt, m);
+      CHECK(m == unhex(r[4]), "free decrypt %s", r[0].c_str());
+      CHECK(zero32(k), "free decrypt must wipe the key");
+      nf += m == unhex(r[4]);
+    }
+    for (auto &r : hs) {
+      auto k = key32(r[1]);
+      Bytes m = unhex(r[4]);
+      const std::optional<Bytes> ad = unhex(r[3]);
+      noise::encrypt(k, std::stoull(r[2]), ad, m);
+      CHECK(m == unhex(r[5]), "free encrypt (AD) %s n=%s", r[0].c_str(), r[2].c_str());
+      k = key32(r[1]);
+      noise::decrypt(k, std::stoull(r[2]), ad, m);
+      CHECK(m == unhex(r[4]), "free decrypt (AD) %s", r[0].c_str());
+      nf += m == unhex(r[4]);
+    }
+    auto k = key32(tr[0][2]);
+    Bytes m = unhex(tr[0][5]);
+    m[m.size() - 1] ^= 1;
+    const Bytes before = m;
+    bool threw = false;
+    try { noise::decrypt(k, std::stoull(tr[0][3]), std::nullopt, m); } catch (const std::invalid_argument &e) {
+      threw = std::string(e.what()) == "Invalid MAC";
+    }
+    CHECK(threw && m == before, "tampered free decrypt: Invalid MAC, buffer untouched");
+    CHECK(zero32(k), "failed free decrypt still wipes the key (noise.cpp:272)");
+    k = key32(tr[0][2]);
+    Bytes tiny = {1, 2};
+    threw = false;
+    try { noise::decrypt(k, 0, std::nullopt, tiny); } catch (const std::invalid_argument &) { threw = true; }
+    CHECK(threw && tiny.size() == 2, "free decrypt of < 16 bytes throws (reference: underflow)");
+    std::printf("free functions: %d/%zu golden round trips ok\n", nf, tr.size() + hs.size());
   }
   std::printf("transport %d/%zu round trips ok\n", n_ok, tr.size());
 }

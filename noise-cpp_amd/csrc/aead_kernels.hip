@@ -12,6 +12,7 @@
 // workgroups, one record per thread; the grid covers nrec.
 #include "chachapoly_device.hpp"
 #include "launchers.hpp"
+#include "mtile_kernel.hpp"
 #include "tile_kernel.hpp"
 
 namespace noise_amd {
@@ -142,6 +143,44 @@ hipError_t launch_aead_uniform(bool decrypt, const uint32_t key[8],
     }
 #undef NOISE_TILE_CASE
 #undef NOISE_TILE_LAUNCH
+  }
+  // any other length up to 16 KiB with 16-byte aligned bases and strides:
+  // the masked tile kernel at the smallest tile capacity >= len
+  // (mtile_kernel.hpp)
+  const bool al = ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out) | in_stride |
+                    out_stride) & 15u) == 0;
+  if (al && ad_len == 0 && len >= 1 && len <= 16384) {
+    TileArgs ta{};
+    ta.key = k;
+    ta.nonce0 = nonce0;
+    ta.in = in;
+    ta.in_stride = in_stride;
+    ta.out = out;
+    ta.out_stride = out_stride;
+    ta.status = status;
+    ta.nrec = nrec;
+    ta.in_place = in == out;
+    ta.len = len;
+    ta.chunk = -1;
+#define NOISE_MTILE(LEN)                                                       \
+    if (len <= LEN) {                                                          \
+      constexpr uint64_t rps = LEN > 2048 ? 64 * 2048 / LEN : 64;              \
+      const dim3 gm((unsigned)((nrec + rps - 1) / rps)), bm(64);               \
+      if (decrypt) hipLaunchKernelGGL((k_aead_mtile<true, LEN, kMTUniform>), gm, bm, 0, stream, ta); \
+      else hipLaunchKernelGGL((k_aead_mtile<false, LEN, kMTUniform>), gm, bm, 0, stream, ta);        \
+      return hipGetLastError();                                                \
+    }
+    NOISE_MTILE(64)
+    NOISE_MTILE(128)
+    NOISE_MTILE(192)
+    NOISE_MTILE(256)
+    NOISE_MTILE(512)
+    NOISE_MTILE(1024)
+    NOISE_MTILE(2048)
+    NOISE_MTILE(4096)
+    NOISE_MTILE(8192)
+    NOISE_MTILE(16384)
+#undef NOISE_MTILE
   }
   const dim3 g = grid_for(nrec), b(kBlock);
   if (decrypt) {

@@ -1,0 +1,665 @@
+// mtile_kernel.hpp -- the masked ("ragged") tile kernel: the LDS-staged AEAD
+// of tile_kernel.hpp for records of ANY length 1 <= len <= L in a tile class
+// of capacity L (the fast paths were keyed to a
+// fixed table of lengths; 1000-, 1400- or 5000-byte records fell to a lane
+// per record).  Same reference semantics: crypto_aead_write / _read
+// (monocypher.c:2899-2929) under the Noise nonce 0^32 || LE64(n)
+// (noise.cpp:207-215), any length (noise.cpp:202-281).
+//
+// Layout: the record's bytes sit in the tile at their own (16-byte aligned)
+// positions, as for an exact record; only the lanes' view is shifted.  A
+// class of capacity L has CV = L / 64 ChaCha chunk slots and PV = L / 16
+// Poly1305 block slots per record, G lanes of CPL chunks / BPL blocks each.
+// A record of C = ceil(len / 64) chunks and P = ceil(len / 16) blocks is
+// RIGHT-aligned in that virtual space:
+//   virtual chunk v  <-> real chunk  v - (CV - C)   (absent when negative)
+//   virtual block v  <-> real block  v - (PV - P)   (absent when negative)
+// so the absent slots are LEADING ones.  A leading absent Poly1305 block reads
+// the tile's zero slot with no 2^128 bit: Horner from h = 0 stays 0 through
+// it, so every lane's partial sum keeps the exact-size weight r^(BPL (G-1-j))
+// and the recombination is tile_kernel.hpp's, unchanged -- no per-record
+// powers.  The real chunk count and block count differ by t = 4C - P in
+// [0, 3] blocks, so a lane's Poly1305 span can start up to 3 blocks into the
+// previous virtual chunk -- the previous lane's last one for j > 0:
+//   encrypt: the lanes first XOR their LAST virtual chunk (into the tile),
+//     then chunks 0, 1, ... with the Poly1305 of chunk k right after the XOR
+//     of chunk k (ChaCha of chunk k + 1 interleaved with it);
+//   decrypt: Poly1305 of chunk k over the ciphertext, the XOR of chunk k - 1
+//     after it (so no ciphertext is overwritten before it is MACed).
+// The last real block's bytes past len are zeroed in the tile before it is
+// MACed (encrypt: the ciphertext tail; decrypt: the tag bytes, after the tag
+// was read out), as the AEAD's zero padding.  The tag sits at byte len: it is
+// read out of (decrypt) / shifted into (encrypt) the two 16-byte pieces it
+// straddles.  Stores: the whole 16-byte pieces of the output, then the
+// partial last piece byte-wise -- no byte past the record's output is
+// written (len + 16 encrypt, len decrypt; Noise wire ct || tag).
+//
+// Reads: the 16-byte aligned pieces holding the record's input bytes are
+// read whole.  A record starts 16-byte aligned (the callers check it), so the
+// last piece ends at most 15 bytes past the input and never crosses a page:
+// those bytes (padding, a neighbour's, the in-place tag) are masked, never
+// used or written.
+//
+// Modes (MT_*):
+//   kMTUniform   one key, nonce0 + i, record i at in + i * in_stride (strides
+//                and bases 16-byte aligned), len = a.len
+//   kMTDesc      descriptor records of one ceiling class (records_kernels.hip)
+//   kMTTail      the tail (len % 1024 bytes past the full 1 KiB segments) of
+//                a long record, encrypt: ciphertext + its Poly1305 sum P_tail
+//                into the SegRec, no tag (k_seg_finalize_w adds the rest)
+//   kMTTailPoly  decrypt, before the tags are known: P_tail of the ciphertext
+//   kMTTailXor   decrypt, after k_seg_finalize_w: plaintext of the tails of
+//                the records whose tag verified (a failed one: nothing in
+//                place, zeros as a copy)
+// The tail modes read r, r^16, r^32 and the key from the record's SegRec
+// (k_seg_prep) instead of a key pass; ChaCha counters continue at 1 + 16 nf.
+#pragma once
+#include "tile_kernel.hpp"
+
+namespace noise_amd {
+
+// two waves per SIMD (<= 256 VGPRs): the masked kernels hold more state
+// than the exact ones and the compiler would otherwise take AGPRs and drop
+// to one wave per SIMD (the CPU emulation build has no such attribute)
+#if defined(NOISE_HIP_EMU)
+#define NOISE_OCC2
+#else
+#define NOISE_OCC2 __attribute__((amdgpu_waves_per_eu(2)))
+#endif
+
+enum MTileMode : int { kMTUniform = 0, kMTDesc = 1, kMTTail = 2, kMTTailPoly = 3, kMTTailXor = 4 };
+
+// 16 bytes at byte offset k (1..15) of the 32-byte little-endian [lo | hi]
+__device__ __forceinline__ uint4 extract16(const uint4 lo, const uint4 hi, uint32_t k) {
+  uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  // word shift by k / 4 (0..3) in two select stages, then a byte funnel
+  const bool s8 = (k & 8u) != 0, s4 = (k & 4u) != 0;
+  uint32_t u[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) u[i] = s8 ? w[i + 2] : w[i];
+  uint32_t v[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) v[i] = s4 ? u[i + 1] : u[i];
+  const uint32_t b = k & 3u;
+  uint4 o;
+  o.x = __builtin_amdgcn_alignbyte(v[1], v[0], b);
+  o.y = __builtin_amdgcn_alignbyte(v[2], v[1], b);
+  o.z = __builtin_amdgcn_alignbyte(v[3], v[2], b);
+  o.w = __builtin_amdgcn_alignbyte(v[4], v[3], b);
+  return o;
+}
+
+// Poly1305 block with a selectable 2^128 bit: hb = 0 and m = 0 on h = 0 is
+// the identity (a leading absent block); hb = 1 is poly_block
+__device__ __forceinline__ void poly_block_hb(Poly1305 &p, uint32_t m0, uint32_t m1, uint32_t m2,
+                                              uint32_t m3, uint32_t hb) {
+  unsigned c;
+  const uint32_t s0 = __builtin_addc(p.h0, m0, 0u, &c);
+  const uint32_t s1 = __builtin_addc(p.h1, m1, c, &c);
+  const uint32_t s2 = __builtin_addc(p.h2, m2, c, &c);
+  const uint32_t s3 = __builtin_addc(p.h3, m3, c, &c);
+  const uint32_t s4 = p.h4 + c + hb;
+  const uint64_t x0 = mad64(s0, p.r0, mad64(s1, p.rr3, mad64(s2, p.rr2, mad64(s3, p.rr1, mad64(s4, p.rr0, 0)))));
+  const uint64_t x1 = mad64(s0, p.r1, mad64(s1, p.r0, mad64(s2, p.rr3, mad64(s3, p.rr2, mad64(s4, p.rr1, 0)))));
+  const uint64_t x2 = mad64(s0, p.r2, mad64(s1, p.r1, mad64(s2, p.r0, mad64(s3, p.rr3, mad64(s4, p.rr2, 0)))));
+  const uint64_t x3 = mad64(s0, p.r3, mad64(s1, p.r2, mad64(s2, p.r1, mad64(s3, p.r0, mad64(s4, p.rr3, 0)))));
+  const uint32_t x4 = __umul24(s4, p.r0lo);
+  const uint32_t u5 = x4 + (uint32_t)(x3 >> 32);
+  const uint32_t q = u5 >> 2;
+  p.h0 = __builtin_addc(q + (q << 2), (uint32_t)x0, 0u, &c);
+  p.h1 = __builtin_addc((uint32_t)x1, (uint32_t)(x0 >> 32), c, &c);
+  p.h2 = __builtin_addc((uint32_t)x2, (uint32_t)(x1 >> 32), c, &c);
+  p.h3 = __builtin_addc((uint32_t)x3, (uint32_t)(x2 >> 32), c, &c);
+  p.h4 = (u5 & 3u) + c;
+}
+
+// The first `n` (1..15) bytes of a 16-byte piece at a 16-byte aligned
+// address: whole dwords, then a short and a byte as needed
+__device__ __forceinline__ void store_head(uint8_t *p, uint4 v, uint32_t n) {
+  store16<false>(p, v, (int)n);
+}
+
+template <bool DECRYPT, int L, int MODE>
+__global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) {
+  using C = TileCfg<L, 256>;
+  constexpr int G = C::G, CPL = C::CPL, BPL = C::BPL, SPR = C::SPR, RPT = C::RPT;
+  constexpr int REC_SLOTS = C::REC_SLOTS, NSLOT = C::NSLOT;
+  constexpr int ZSLOT = NSLOT, JSLOT = NSLOT + 1;  // zero slot, junk slot (absent XOR writes)
+  constexpr bool TAIL = MODE >= kMTTail;
+  constexpr bool KEYED = MODE != kMTUniform;
+  constexpr bool DO_XOR = MODE != kMTTailPoly;
+  constexpr bool DO_POLY = MODE != kMTTailXor;
+  constexpr bool TAG_IN = DECRYPT && !TAIL;   // input ct || tag, check the tag
+  constexpr bool TAG_OUT = !DECRYPT && !TAIL; // output ct || tag
+  constexpr bool POLY_PRE = DECRYPT;          // Poly1305 over the input (before the XOR)
+  static_assert(!TAIL || L == 1024, "tails are cut to 1 KiB units");
+  static_assert(MODE != kMTTail || !DECRYPT, "the fused tail pass is encrypt's");
+  static_assert(MODE < kMTTailPoly || DECRYPT, "the split tail passes are decrypt's");
+  constexpr int OPR = TAG_OUT ? SPR + 1 : SPR;  // output pieces of a full record
+  constexpr int KPR = SPR / 64;                 // KiB per record (L >= 1024)
+  constexpr bool WHOLE_KIB = SPR % 64 == 0;
+  // records per super-tile: 64 (one key lane each), at most 128 KiB for
+  // classes of 4 KiB and up (so that batches of large records make waves)
+  constexpr int RPS = L > 2048 ? 64 * 2048 / L : 64;
+  constexpr int NTS = RPS / RPT;
+  static_assert(NTS >= 1 && RPS % RPT == 0, "super-tile shape");
+  __shared__ uint4 lds[NSLOT + 2];
+  uint4 *lb = lds;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t rho = lane / G, j = lane % G;
+  if (lane == 0) lds[ZSLOT] = make_uint4(0u, 0u, 0u, 0u);  // never overwritten
+  uint32_t gl[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) gl[i] = swz<256>(64u * i + lane) - 64u * i;
+
+  // the work list
+  uint64_t nrec = a.nrec, dbase = 0;
+  if (MODE == kMTDesc) {
+    dbase = a.cls_base[a.cls];
+    nrec = a.counts[a.cls];
+  } else if (TAIL) {
+    const uint64_t nall = *a.ntails;
+    uint64_t lo = 0, hi = nall;
+    if (a.chunk >= 0 && a.tail_split) {
+      lo = a.tail_split[a.chunk] < nall ? a.tail_split[a.chunk] : nall;
+      hi = a.tail_split[a.chunk + 1] < nall ? a.tail_split[a.chunk + 1] : nall;
+    }
+    dbase = lo;
+    nrec = hi > lo ? hi - lo : 0;
+  }
+  const uint64_t nlong = TAIL ? *a.nlong : 0ull;
+  uint32_t kuni[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) kuni[i] = a.key.w[i];
+  const uint8_t *in = a.in;
+  uint8_t *out = a.out;
+
+#pragma unroll 1
+  for (uint64_t super0 = (uint64_t)blockIdx.x * RPS; super0 < nrec;
+       super0 += (uint64_t)gridDim.x * RPS) {
+    // ---- key pass: lane l -> record super0 + l --------------------------
+    uint32_t own_k[8], own_nlo = 0, own_nhi = 0, own_len = 0, own_cb = 0, own_di = 0, own_q = 0;
+    uint32_t own_in_lo = 0, own_in_hi = 0, own_out_lo = 0, own_out_hi = 0;
+    bool own_bad = false, own_inplace = false, own_ok = true;
+    uint32_t kr[4] = {0u, 0u, 0u, 0u}, kss[4] = {0u, 0u, 0u, 0u};
+    F26 pw[C::LOG2G > 0 ? C::LOG2G : 1];
+#pragma unroll
+    for (int b = 0; b < (C::LOG2G > 0 ? C::LOG2G : 1); ++b)
+#pragma unroll
+      for (int i = 0; i < 5; ++i) pw[b].a[i] = 0u;
+    {
+      const uint64_t rec = super0 + lane;
+      const bool have = rec < nrec && lane < (uint32_t)RPS;
+      uint64_t n = 0, ioff = 0, ooff = 0;
+      uint32_t ki = 0;
+      if (MODE == kMTUniform) {
+        n = a.nonce0 + rec;
+        ioff = rec * a.in_stride;
+        ooff = rec * a.out_stride;
+        own_len = have ? a.len : 0u;
+      } else if (MODE == kMTDesc) {
+        if (have) {
+          own_di = a.idx[dbase + rec];
+          const noise_gpu_record d = a.recs[own_di];
+          ki = d.key_idx;
+          n = d.nonce;
+          ioff = d.in_off;
+          ooff = d.out_off;
+          own_len = d.len;
+        }
+      } else {  // tails: the long record's SegRec
+        if (have) {
+          own_q = a.tails[dbase + rec];
+          if (own_q < nlong) {
+            const SegRec &R = a.rt[own_q];
+            const uint32_t nf = R.nfull;
+            n = R.nonce;
+            ioff = R.in_off + 1024ull * nf;
+            ooff = R.out_off + 1024ull * nf;
+            own_len = R.len - 1024u * nf;
+            own_cb = 16u * nf;
+            if (MODE == kMTTailXor) own_ok = R.ok != 0u;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) own_k[i] = R.k[i];
+            if (DO_POLY) {
+#pragma unroll
+              for (int i = 0; i < 4; ++i) kr[i] = R.r[i];
+              // G = 4 lanes: r^16, r^32 (k_seg_prep)
+#pragma unroll
+              for (int b = 0; b < C::LOG2G; ++b) {
+                pw[b].a[0] = R.pwlo[b][0]; pw[b].a[1] = R.pwlo[b][1];
+                pw[b].a[2] = R.pwlo[b][2]; pw[b].a[3] = R.pwlo[b][3]; pw[b].a[4] = R.pwhi[b];
+              }
+            }
+          } else {
+            own_len = 0;  // beyond the segment scratch: the generic kernel has it
+          }
+        }
+      }
+      own_in_lo = (uint32_t)ioff; own_in_hi = (uint32_t)(ioff >> 32);
+      own_out_lo = (uint32_t)ooff; own_out_hi = (uint32_t)(ooff >> 32);
+      own_inplace = in + ioff == out + ooff;
+      own_nlo = (uint32_t)n;
+      own_nhi = (uint32_t)(n >> 32);
+      if (MODE == kMTDesc) {
+        own_bad = ki >= a.nkeys;
+        if (own_bad) ki = 0;
+        const u32x4 *kp = reinterpret_cast<const u32x4 *>(a.keys + 32ull * ki);
+        const u32x4 ka = __builtin_nontemporal_load(kp), kb = __builtin_nontemporal_load(kp + 1);
+        own_k[0] = ka.x; own_k[1] = ka.y; own_k[2] = ka.z; own_k[3] = ka.w;
+        own_k[4] = kb.x; own_k[5] = kb.y; own_k[6] = kb.z; own_k[7] = kb.w;
+        own_bad = own_bad || (ka.x | ka.y | ka.z | ka.w | kb.x | kb.y | kb.z | kb.w) == 0u;
+      } else if (MODE == kMTUniform) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) own_k[i] = kuni[i];
+      } else if (!(have && own_q < nlong)) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) own_k[i] = 0u;
+      }
+    }
+    // input pieces of the record (decrypt: ct || tag, encrypt: pt / a tail)
+    const uint32_t own_np = TAG_IN ? (own_len + 31u) >> 4 : (own_len + 15u) >> 4;
+
+    // the first tile's DMA goes out before the key block and lands meanwhile
+    auto load_tile = [&](uint64_t rec0, uint32_t t_rpt) {
+      const uint64_t left = nrec - rec0;
+      const uint32_t nv = left < (uint64_t)RPT ? (uint32_t)left : (uint32_t)RPT;
+      constexpr int IN_SLOTS = TAG_IN ? NSLOT : REC_SLOTS;
+      if constexpr (WHOLE_KIB) {
+        // instruction q: KiB q % KPR of record q / KPR, a wave-uniform base
+#pragma unroll
+        for (int q = 0; q < REC_SLOTS / 64; ++q) {
+          const uint32_t kl = t_rpt + (uint32_t)q / KPR;
+          const uint32_t np = (uint32_t)__builtin_amdgcn_readlane((int)own_np, (int)kl);
+          const uint32_t kib = 64u * ((uint32_t)q % KPR);
+          if ((uint32_t)(q / KPR) < nv && kib < np) {
+            const uint64_t off = join64((uint32_t)__builtin_amdgcn_readlane((int)own_in_hi, (int)kl),
+                                        (uint32_t)__builtin_amdgcn_readlane((int)own_in_lo, (int)kl)) +
+                                 1024ull * ((uint32_t)q % KPR);
+            const uint32_t pc = kib + glq<256>(gl, q);
+            if (pc < np) lds_dma16_s<true>(in + off, 16u * glq<256>(gl, q), (lds_void *)(NOISE_LDS3(lds) + 64 * q));
+          }
+        }
+        if (TAG_IN) {  // piece SPR of record r (the tag of a full-size record) -> tag slot r
+          const uint32_t r = lane < (uint32_t)RPT ? lane : 0u;
+          const uint32_t src = t_rpt + r;
+          const uint64_t off = join64((uint32_t)__shfl((int)own_in_hi, (int)src), (uint32_t)__shfl((int)own_in_lo, (int)src));
+          const uint32_t np = (uint32_t)__shfl((int)own_np, (int)src);
+          if (lane < (uint32_t)RPT && lane < nv && np > (uint32_t)SPR)
+            lds_dma16_v<true>(in + off + 16u * SPR, (lds_void *)(NOISE_LDS3(lds) + REC_SLOTS));
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < (IN_SLOTS + 63) / 64; ++q) {
+          const uint32_t s = 64u * q + lane;
+          uint32_t r, p;
+          if (s < (uint32_t)REC_SLOTS) {
+            const uint32_t g = swz<256>(s);
+            r = g / SPR;
+            p = g % SPR;
+          } else {  // tag slots
+            r = s - REC_SLOTS;
+            p = SPR;
+          }
+          const uint32_t src = t_rpt + (r < (uint32_t)RPT ? r : 0u);
+          const uint64_t off = join64((uint32_t)__shfl((int)own_in_hi, (int)src), (uint32_t)__shfl((int)own_in_lo, (int)src));
+          const uint32_t np = (uint32_t)__shfl((int)own_np, (int)src);
+          if (s < (uint32_t)IN_SLOTS && r < nv && p < np)
+            lds_dma16_v<true>(in + off + 16u * p, (lds_void *)(NOISE_LDS3(lds) + 64 * q));
+        }
+      }
+    };
+    load_tile(super0, 0u);
+
+    if (!TAIL) {  // ChaCha block 0: r, s; G > 1: r^BPL, r^(2 BPL), ...
+      uint32_t otk[16];
+      chacha20_block(own_k, 0u, own_nlo, own_nhi, otk);
+      kr[0] = otk[0] & 0x0fffffffu;
+      kr[1] = otk[1] & 0x0ffffffcu;
+      kr[2] = otk[2] & 0x0ffffffcu;
+      kr[3] = otk[3] & 0x0ffffffcu;
+      kss[0] = otk[4]; kss[1] = otk[5]; kss[2] = otk[6]; kss[3] = otk[7];
+      if (G > 1) {
+        F26 x = to26(kr[0], kr[1], kr[2], kr[3], 0u);
+#pragma unroll
+        for (int b = 0; b < C::LOG2BPL; ++b) x = mul26(x, x);
+        pw[0] = x;
+#pragma unroll
+        for (int b = 1; b < C::LOG2G; ++b) pw[b] = mul26(pw[b - 1], pw[b - 1]);
+      }
+    }
+
+#pragma unroll 1
+    for (int t = 0; t < NTS; ++t) {
+      const uint64_t rec0 = super0 + (uint64_t)t * RPT;
+      if (rec0 >= nrec) break;
+      const uint32_t nv = (nrec - rec0) < (uint64_t)RPT ? (uint32_t)(nrec - rec0) : (uint32_t)RPT;
+      wait_vmem();
+      wave_lds_fence();
+      const uint32_t src = (uint32_t)t * RPT + rho;  // key lane of my record
+      const bool valid = rho < nv;
+      // ---- this lane's record ------------------------------------------
+      const uint32_t rlen = (uint32_t)__shfl((int)own_len, (int)src);
+      const uint32_t P = (rlen + 15u) >> 4, Cc = (rlen + 63u) >> 6;
+      const uint32_t F = rlen >> 4, sb = rlen & 15u;  // whole pieces, bytes in the last one
+      const int D = (int)(L / 16) - (int)P, dc = (int)(L / 64) - (int)Cc;
+      const uint32_t rbase = rho * SPR;
+      auto pslot = [&](uint32_t i) -> uint32_t {  // record piece i (0 .. SPR) -> slot
+        return i < (uint32_t)SPR ? swz<256>(rbase + i) : (uint32_t)REC_SLOTS + rho;
+      };
+      Poly1305 p;
+      p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0u;
+      p.r0 = p.r1 = p.r2 = p.r3 = 0u;
+      p.s0 = p.s1 = p.s2 = p.s3 = 0u;
+      if (DO_POLY) {
+        p.r0 = __shfl(kr[0], src); p.r1 = __shfl(kr[1], src);
+        p.r2 = __shfl(kr[2], src); p.r3 = __shfl(kr[3], src);
+        p.s0 = __shfl(kss[0], src); p.s1 = __shfl(kss[1], src);
+        p.s2 = __shfl(kss[2], src); p.s3 = __shfl(kss[3], src);
+      }
+      p.rr0 = (p.r0 >> 2) * 5u;
+      p.rr1 = p.r1 + (p.r1 >> 2);
+      p.rr2 = p.r2 + (p.r2 >> 2);
+      p.rr3 = p.r3 + (p.r3 >> 2);
+      p.r0lo = p.r0 & 3u;
+      uint32_t kt[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) kt[i] = DO_XOR ? (KEYED ? (uint32_t)__shfl((int)own_k[i], (int)src) : kuni[i]) : 0u;
+      uint32_t n_lo = 0u, n_hi = 0u, cbase = 1u;
+      if (DO_XOR) {
+        if (KEYED) {
+          n_lo = (uint32_t)__shfl((int)own_nlo, (int)src);
+          n_hi = (uint32_t)__shfl((int)own_nhi, (int)src);
+        } else {
+          const uint64_t n = a.nonce0 + rec0 + rho;
+          n_lo = (uint32_t)n;
+          n_hi = (uint32_t)(n >> 32);
+        }
+        if (TAIL) cbase += (uint32_t)__shfl((int)own_cb, (int)src);
+      }
+      const bool bad_key = MODE == kMTDesc && __shfl((int)own_bad, (int)src) != 0;
+
+      // ---- decrypt: the tag out of the tile, zero padding for the MAC ----
+      uint4 want = make_uint4(0u, 0u, 0u, 0u);
+      if (TAG_IN) {
+        const uint4 A = lb[pslot(F)];
+        const uint4 B = lb[sb ? pslot(F + 1u) : (uint32_t)ZSLOT];
+        want = sb ? extract16(A, B, sb) : A;
+        wave_lds_fence();
+        if (sb && j == 0 && valid) lb[pslot(F)] = mask_bytes(A, (int)sb);
+        wave_lds_fence();
+      } else if (POLY_PRE && DO_POLY) {  // tail Poly1305 pass: zero the bytes past the tail
+        const uint4 A = lb[pslot(F)];
+        wave_lds_fence();  // (wave-wide: no barrier inside lane-divergent code)
+        if (sb && j == 0 && valid) lb[pslot(F)] = mask_bytes(A, (int)sb);
+        wave_lds_fence();
+      }
+
+      // ---- ChaCha20 XOR and Poly1305, right-aligned (see the top) ------
+      const int rc0 = (int)(CPL * j) - dc;          // real chunk of my virtual chunk 0
+      const int rb0 = (int)(BPL * j) - D;           // real block of my virtual block 0
+      ChaPre pre{};
+      if (DO_XOR) pre = chacha_pre(kt, n_lo, n_hi);
+      auto keystream = [&](int vc, uint32_t ks[16]) {
+        chacha20_block_pre(kt, cbase + (uint32_t)(rc0 + vc), pre, n_lo, n_hi, ks);
+      };
+      auto xor_chunk = [&](int vc, const uint32_t ks[16]) {
+        const int c = rc0 + vc;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t slot = c >= 0 ? swz<256>(rbase + 4u * (uint32_t)c + (uint32_t)q) : (uint32_t)JSLOT;
+          const uint4 v = lb[slot];
+          uint4 o;
+          o.x = v.x ^ ks[4 * q + 0];
+          o.y = v.y ^ ks[4 * q + 1];
+          o.z = v.z ^ ks[4 * q + 2];
+          o.w = v.w ^ ks[4 * q + 3];
+          lb[slot] = o;
+        }
+      };
+      auto poly_chunk = [&](int vc) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int b = rb0 + 4 * vc + q;
+          const uint32_t slot = b >= 0 ? swz<256>(rbase + (uint32_t)b) : (uint32_t)ZSLOT;
+          const uint4 v = lb[slot];
+          poly_block_hb(p, v.x, v.y, v.z, v.w, b >= 0 ? 1u : 0u);
+        }
+      };
+      if (!DO_XOR) {  // tail Poly1305 pass
+#pragma unroll
+        for (int kk = 0; kk < CPL; ++kk) poly_chunk(kk);
+      } else if (!DO_POLY) {  // tail plaintext pass
+        uint32_t ks[16];
+        keystream(0, ks);
+#pragma unroll
+        for (int kk = 0; kk < CPL; ++kk) {
+          uint32_t ksn[16];
+          if (kk + 1 < CPL) keystream(kk + 1, ksn);
+          xor_chunk(kk, ks);
+          if (kk + 1 < CPL) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) ks[i] = ksn[i];
+          }
+        }
+      } else if (POLY_PRE) {
+        // decrypt: Poly1305 of chunk kk over the ciphertext, then the XOR of
+        // chunk kk - 1 (chunk kk's MAC may reach 3 blocks into chunk kk - 1)
+        uint32_t ksp[16];
+#pragma unroll
+        for (int kk = 0; kk < CPL; ++kk) {
+          uint32_t ksc[16];
+          keystream(kk, ksc);
+          poly_chunk(kk);
+          if (kk > 0) xor_chunk(kk - 1, ksp);
+#pragma unroll
+          for (int i = 0; i < 16; ++i) ksp[i] = ksc[i];
+        }
+        wave_lds_fence();  // every lane's last MAC read (the next lane's chunk 0) before this write
+        xor_chunk(CPL - 1, ksp);
+      } else {
+        // encrypt: the last chunk first (the next lane's first MAC blocks
+        // may lie in it), its tail bytes zeroed; then chunk kk, its MAC
+        {
+          uint32_t ksl[16];
+          keystream(CPL - 1, ksl);
+          xor_chunk(CPL - 1, ksl);
+        }
+        wave_lds_fence();
+        if (sb && j == (uint32_t)G - 1u && valid) lb[pslot(F)] = mask_bytes(lb[pslot(F)], (int)sb);
+        wave_lds_fence();
+        uint32_t ks[16];
+        if (CPL > 1) keystream(0, ks);
+#pragma unroll
+        for (int kk = 0; kk < CPL; ++kk) {
+          uint32_t ksn[16];
+          if (kk + 1 < CPL - 1) keystream(kk + 1, ksn);
+          if (kk < CPL - 1) xor_chunk(kk, ks);
+          poly_chunk(kk);
+          if (kk + 1 < CPL - 1) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) ks[i] = ksn[i];
+          }
+        }
+      }
+
+      // ---- recombination: sum_j acc_j r^(BPL (G-1-j)) (tile_kernel.hpp) --
+      if (DO_POLY && G > 1) {
+        F26 h = to26(p.h0, p.h1, p.h2, p.h3, p.h4);
+        const uint32_t m = (uint32_t)G - 1u - j;
+#pragma unroll
+        for (int b = 0; b < C::LOG2G; ++b) {
+          F26 f;
+          const bool use = (m >> b) & 1u;
+#pragma unroll
+          for (int i = 0; i < 5; ++i) {
+            const uint32_t w = __shfl(pw[b].a[i], src);
+            f.a[i] = use ? w : (i == 0 ? 1u : 0u);
+          }
+          h = mul26(h, f);
+        }
+#pragma unroll
+        for (int b = 0; b < C::LOG2G; ++b) {
+          if (b == 4) carry26(h);
+#pragma unroll
+          for (int i = 0; i < 5; ++i) h.a[i] += __shfl_xor(h.a[i], 1 << b);
+        }
+        carry26(h);
+        carry26(h);
+        from26(h, p.h0, p.h1, p.h2, p.h3, p.h4);
+      }
+      uint32_t tag[4] = {0u, 0u, 0u, 0u};
+      if (!TAIL) {
+        poly_block(p, 0u, 0u, rlen, 0u);  // LE64(ad_len = 0) || LE64(len)
+        poly_final(p, tag);
+      }
+
+      // ---- outcome per record --------------------------------------------
+      uint64_t fail_mask = 0;  // bit r * G: record r of this tile is not output as computed
+      const uint64_t badk_mask = __ballot(j == 0 && bad_key);
+      fail_mask = badk_mask;
+      const uint32_t rec_di = MODE == kMTDesc ? (uint32_t)__shfl((int)own_di, (int)src) : 0u;
+      const bool rec_inplace = __shfl((int)own_inplace, (int)src) != 0;
+      const uint64_t inpl_mask = __ballot(j == 0 && rec_inplace);
+      if (TAG_IN) {
+        const uint32_t diff = (want.x ^ tag[0]) | (want.y ^ tag[1]) | (want.z ^ tag[2]) | (want.w ^ tag[3]);
+        fail_mask |= __ballot(j == 0 && valid && diff != 0u);
+        if (j == 0 && valid) {
+          const uint64_t si = MODE == kMTDesc ? (uint64_t)rec_di : rec0 + rho;
+          a.status[si] = bad_key ? 2u : (diff ? 1u : 0u);
+        }
+      } else if (MODE == kMTTailXor) {  // the record's tag failed: its tail is not output
+        const bool rec_ok = __shfl((int)own_ok, (int)src) != 0;  // every lane shuffles
+        fail_mask |= __ballot(j == 0 && valid && !rec_ok);
+      }
+      {
+        // P_tail -> the SegRec, for k_seg_finalize_w (shuffle outside divergent code)
+        const uint32_t q = TAIL ? (uint32_t)__shfl((int)own_q, (int)src) : 0u;
+        if (TAIL && DO_POLY && j == 0 && valid && rlen != 0u) {  // rlen 0: past the scratch
+          SegRec &R = const_cast<SegRec &>(a.rt[q]);
+          R.ptail[0] = p.h0; R.ptail[1] = p.h1; R.ptail[2] = p.h2; R.ptail[3] = p.h3;
+          R.ptail[4] = p.h4;
+        }
+      }
+      if (TAG_OUT && j == 0 && valid) {  // the tag at byte rlen of the output image
+        const uint4 T = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+        if (sb == 0u) {
+          lb[pslot(F)] = T;
+        } else {
+          const uint4 Z = make_uint4(0u, 0u, 0u, 0u);
+          const uint4 A = lb[pslot(F)];  // ciphertext, zero past rlen
+          const uint4 lo = extract16(Z, T, 16u - sb), hi = extract16(T, Z, 16u - sb);
+          lb[pslot(F)] = make_uint4(A.x | lo.x, A.y | lo.y, A.z | lo.z, A.w | lo.w);
+          lb[pslot(F + 1u)] = hi;
+        }
+      }
+      wave_lds_fence();
+      if (!DO_XOR) {  // tail Poly1305 pass: nothing to store; the next tile's DMA
+        if (t + 1 < NTS && rec0 + RPT < nrec) {
+          wait_lds();
+          wave_lds_fence();
+          load_tile(rec0 + RPT, (uint32_t)(t + 1) * RPT);
+        }
+        continue;
+      }
+
+      // ---- gather the outputs, next tile's DMA, stores ------------------
+      // output bytes of record r: len + 16 (encrypt with tag) or len.  The
+      // whole pieces go out as 16-byte stores, in NPART parts (fewer pieces
+      // live in registers); the next tile's DMA overwrites the tile, so it
+      // is issued after the last part's gather, before that part's stores.
+      constexpr int NOUT = WHOLE_KIB ? (REC_SLOTS / 64 + (TAG_OUT ? 1 : 0)) : (RPT * OPR + 63) / 64;
+      constexpr int NPART = NOUT > 8 ? 2 : 1;
+      constexpr int NQ = (NOUT + NPART - 1) / NPART;
+      const bool full = nv == (uint32_t)RPT;
+#pragma unroll
+      for (int part = 0; part < NPART; ++part) {
+        uint4 ov[NQ];
+        bool st[NQ];
+        uint64_t dst[NQ];
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq) {
+          const int q = part * NQ + qq;
+          st[qq] = false;
+          dst[qq] = 0;
+          ov[qq] = make_uint4(0u, 0u, 0u, 0u);
+          if (q >= NOUT) break;
+          uint32_t r, pc, slot;
+          bool ok;
+          if (WHOLE_KIB && q < REC_SLOTS / 64) {  // KiB q % KPR of record q / KPR
+            r = (uint32_t)q / KPR;
+            pc = 64u * ((uint32_t)q % KPR) + lane;
+            slot = swz<256>(64u * q + lane);
+            ok = true;
+          } else if (WHOLE_KIB) {  // the tag slots (piece SPR), lane r -> record r
+            r = lane < (uint32_t)RPT ? lane : 0u;
+            pc = SPR;
+            slot = REC_SLOTS + r;
+            ok = lane < (uint32_t)RPT;
+          } else {
+            const uint32_t g = 64u * q + lane;
+            r = g / OPR;
+            pc = g % OPR;
+            ok = (RPT * OPR) % 64 == 0 || g < (uint32_t)(RPT * OPR);
+            if (!ok) r = 0;
+            slot = pc < (uint32_t)SPR ? swz<256>(r * SPR + pc) : (uint32_t)REC_SLOTS + r;
+          }
+          const uint32_t kl = (uint32_t)t * RPT + r;
+          uint32_t ln, olo, ohi;
+          if (WHOLE_KIB && q < REC_SLOTS / 64) {  // one record per instruction: wave-uniform
+            ln = (uint32_t)__builtin_amdgcn_readlane((int)own_len, (int)kl);
+            olo = (uint32_t)__builtin_amdgcn_readlane((int)own_out_lo, (int)kl);
+            ohi = (uint32_t)__builtin_amdgcn_readlane((int)own_out_hi, (int)kl);
+          } else {
+            ln = (uint32_t)__shfl((int)own_len, (int)kl);
+            olo = (uint32_t)__shfl((int)own_out_lo, (int)kl);
+            ohi = (uint32_t)__shfl((int)own_out_hi, (int)kl);
+          }
+          const uint32_t nfo = (ln + (TAG_OUT ? 16u : 0u)) >> 4;  // whole output pieces
+          st[qq] = ok && (full || r < nv) && pc < nfo;
+          dst[qq] = join64(ohi, olo) + 16ull * pc;
+          ov[qq] = lb[slot];
+          if ((fail_mask >> (r * G)) & 1u) {  // not output as computed (rare)
+            const bool bk = ((badk_mask >> (r * G)) & 1u) != 0;
+            const bool inpl = ((inpl_mask >> (r * G)) & 1u) != 0;
+            st[qq] = st[qq] && DECRYPT && !inpl && !bk;
+            ov[qq] = make_uint4(0u, 0u, 0u, 0u);
+          }
+        }
+        // the partial last piece of record `lane` (read before the DMA)
+        uint4 pv = make_uint4(0u, 0u, 0u, 0u);
+        uint32_t pn = 0u;
+        uint64_t pdst = 0;
+        if (part == NPART - 1) {
+          const uint32_t r = lane < (uint32_t)RPT ? lane : 0u;
+          const uint32_t kl = (uint32_t)t * RPT + r;
+          const uint32_t ln = (uint32_t)__shfl((int)own_len, (int)kl);
+          const uint32_t olo = (uint32_t)__shfl((int)own_out_lo, (int)kl);
+          const uint32_t ohi = (uint32_t)__shfl((int)own_out_hi, (int)kl);
+          const uint32_t ob = ln + (TAG_OUT ? 16u : 0u);
+          const uint32_t pp = ob >> 4;  // its piece index
+          pn = ob & 15u;
+          const uint32_t slot = pp < (uint32_t)SPR ? swz<256>(r * SPR + pp) : (uint32_t)REC_SLOTS + r;
+          pv = lb[pn ? slot : (uint32_t)ZSLOT];
+          if (!(lane < (uint32_t)RPT && lane < nv)) pn = 0u;
+          if ((fail_mask >> (r * G)) & 1u) {
+            const bool bk = ((badk_mask >> (r * G)) & 1u) != 0;
+            const bool inpl = ((inpl_mask >> (r * G)) & 1u) != 0;
+            if (!DECRYPT || inpl || bk) pn = 0u;
+            pv = make_uint4(0u, 0u, 0u, 0u);
+          }
+          pdst = join64(ohi, olo) + 16ull * pp;
+          wait_lds();  // every LDS read of this tile done
+          wave_lds_fence();
+          if (t + 1 < NTS && rec0 + RPT < nrec) load_tile(rec0 + RPT, (uint32_t)(t + 1) * RPT);
+        }
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq)
+          if (st[qq]) store16<true>(out + dst[qq], ov[qq], 16);
+        if (pn) store_head(out + pdst, pv, pn);
+      }
+    }
+  }
+}
+
+}  // namespace noise_amd

@@ -34,16 +34,19 @@
 
 #include "chachapoly_device.hpp"
 #include "launchers.hpp"
+#include "mtile_kernel.hpp"
 #include "noise_amd/dev_mem.hpp"
 #include "tile_kernel.hpp"
 
 namespace noise_amd {
 
 constexpr int kGenBlock = 256;
-constexpr int kNumTileCls = 10;           // 64 128 192 256 512 1024 2048 4096 8192 16384
-constexpr int kClsLong = kNumTileCls;     // segmented long records
-constexpr int kClsGeneric = kNumTileCls + 1;
-constexpr int kNumCls = kNumTileCls + 2;
+constexpr int kNumTileCls = 10;           // exactly 64 128 192 256 512 1024 2048 4096 8192 16384
+constexpr int kMCls0 = kNumTileCls;       // the masked (ragged) classes: any other length up to
+constexpr int kNumMCls = 10;              //   the same ten capacities (mtile_kernel.hpp)
+constexpr int kClsLong = kMCls0 + kNumMCls;  // segmented long records (> 16 KiB)
+constexpr int kClsGeneric = kClsLong + 1;
+constexpr int kNumCls = kClsLong + 2;
 constexpr int kColSegs = kNumCls;         // classifier column: full segments
 constexpr int kColTails = kNumCls + 1;    // classifier column: long records with a tail
 constexpr int kColFin0 = kNumCls + 2;     // classifier columns: long records by
@@ -66,7 +69,7 @@ constexpr unsigned long long kChunkW = NOISE_CHUNK_W;  // chunk c >= 1 : chunk 0
 #define NOISE_CHUNK_MIN 65536
 #endif
 constexpr uint64_t kChunkMinRecords = NOISE_CHUNK_MIN;  // smaller batches: one chunk
-constexpr int kHdrWords = kSegChunks <= 4 ? 64 : 256;    // scratch header: 512 B (2 KiB)
+constexpr int kHdrWords = kSegChunks <= 4 ? 128 : 256;    // scratch header: 1 KiB (2 KiB)
 // finalize lanes per long record
 #ifndef NOISE_FIN_W
 #define NOISE_FIN_W 4
@@ -149,7 +152,16 @@ __device__ __forceinline__ int record_class(const noise_gpu_record &d, const uin
     case 16384: return 9;
     default: break;
   }
-  return (d.len >= 1024u && d.len <= kLongMax) ? kClsLong : kClsGeneric;
+  // every other length up to 16 KiB: the masked tile class of the smallest
+  // capacity that holds it -- the record still sits whole in one wave's
+  // tile, so decrypt checks its tag there and reads the ciphertext once
+  if (d.len <= 16384u) {
+    const uint32_t n = d.len;
+    const int c = n <= 64u ? 0 : n <= 128u ? 1 : n <= 192u ? 2 : n <= 256u ? 3 : n <= 512u ? 4
+                : n <= 1024u ? 5 : n <= 2048u ? 6 : n <= 4096u ? 7 : n <= 8192u ? 8 : 9;
+    return kMCls0 + c;
+  }
+  return d.len <= kLongMax ? kClsLong : kClsGeneric;
 }
 
 // device header of the scratch buffer
@@ -474,95 +486,6 @@ __global__ __launch_bounds__(64) void k_seg_prep(const uint8_t *__restrict__ key
     for (int m = 0; m < 3; ++m) {
       *reinterpret_cast<u32x4 *>(R.pwlo[m]) = u32x4{pw[m].a[0], pw[m].a[1], pw[m].a[2], pw[m].a[3]};
       R.pwhi[m] = pw[m].a[4];
-    }
-  }
-}
-
-// k_seg_tail: lane per tail (a long record's len % 1024 bytes past its last
-// full segment; ChaCha counters from 1 + 16 nfull), in one of three passes:
-//   kTailFused (encrypt): encrypts the tail and leaves its Poly1305 sum
-//     P_tail (Horner from 0 over the tail's ciphertext blocks, the last one
-//     zero padded) in the SegRec;
-//   kTailPoly (decrypt, before the tag is known): P_tail of the ciphertext
-//     only -- nothing is written to the output;
-//   kTailXor (decrypt, after k_seg_finalize_w): the plaintext of a tail whose
-//     record verified; a failed record's tail is left alone (in place) or
-//     zeroed (copy), as crypto_aead_read leaves a failed record's output.
-enum TailPass : int { kTailFused = 0, kTailPoly = 1, kTailXor = 2 };
-template <bool DECRYPT, int PASS>
-__global__ __launch_bounds__(64) void k_seg_tail(const uint32_t *__restrict__ tails,
-                                                 SegRec *rt, const RecHdr *hdr,
-                                                 const uint8_t *in, uint8_t *out, int chunk) {
-  static_assert(PASS == kTailFused || DECRYPT, "split tail passes are decrypt's");
-  constexpr bool XOR = PASS != kTailPoly, POLY = PASS != kTailXor;
-  const uint64_t nall = hdr->counts[kColTails], nlong = hdr->nlong;
-  uint64_t t0 = 0, n = nall;  // chunk c: the tails [tsplit[c], tsplit[c + 1])
-  if (chunk >= 0) {
-    const uint64_t lo = hdr->tsplit[chunk], hi = hdr->tsplit[chunk + 1];
-    t0 = lo < nall ? lo : nall;
-    n = hi < nall ? hi : nall;
-  }
-#pragma unroll 1
-  for (uint64_t t = t0 + (uint64_t)blockIdx.x * 64 + threadIdx.x; t < n;
-       t += (uint64_t)gridDim.x * 64) {
-    const uint32_t q = tails[t];
-    if (q >= nlong) continue;  // beyond the segment scratch: generic kernel
-    SegRec &R = rt[q];
-    const uint32_t nf = R.nfull, tb = R.len - 1024u * nf;
-    const uint8_t *src = in + R.in_off + 1024ull * nf;
-    uint8_t *dst = out + R.out_off + 1024ull * nf;
-    if (PASS == kTailXor && !R.ok) {  // the tag failed: no plaintext leaves
-      if (in + R.in_off != out + R.out_off)
-        for (uint32_t off = 0; off < tb; off += 16) {
-          const int nb = tb - off >= 16u ? 16 : (int)(tb - off);
-          if (nb == 16) store16<true>(dst + off, make_uint4(0u, 0u, 0u, 0u), 16);
-          else store16<false>(dst + off, make_uint4(0u, 0u, 0u, 0u), nb);
-        }
-      continue;
-    }
-    uint32_t k[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) k[i] = XOR ? R.k[i] : 0u;
-    Poly1305 p;
-    p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0u;
-    if (POLY) {
-      p.r0 = R.r[0]; p.r1 = R.r[1]; p.r2 = R.r[2]; p.r3 = R.r[3];
-      p.rr0 = (p.r0 >> 2) * 5u;
-      p.rr1 = p.r1 + (p.r1 >> 2);
-      p.rr2 = p.r2 + (p.r2 >> 2);
-      p.rr3 = p.r3 + (p.r3 >> 2);
-      p.r0lo = p.r0 & 3u;
-    }
-    const uint32_t n_lo = (uint32_t)R.nonce, n_hi = (uint32_t)(R.nonce >> 32);
-#pragma unroll 1
-    for (uint32_t off = 0; off < tb; off += 64) {
-      uint32_t ks[16];
-      if (XOR) chacha20_block(k, 1u + 16u * nf + (off >> 6), n_lo, n_hi, ks);
-      uint4 v[4];
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {  // the chunk's loads first (independent)
-        const int m = (int)(tb - off) - 16 * w;
-        const int nb = m >= 16 ? 16 : (m > 0 ? m : 0);
-        v[w] = nb == 16 ? load16<true>(src + off + 16 * w, 16)
-                        : load16<false>(src + off + 16 * w, nb);
-      }
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        const int m = (int)(tb - off) - 16 * w;
-        if (m <= 0) break;
-        const int nb = m >= 16 ? 16 : m;
-        if (POLY && DECRYPT) poly_block(p, v[w].x, v[w].y, v[w].z, v[w].w);
-        if (!XOR) continue;
-        const uint4 o = mask_bytes(make_uint4(v[w].x ^ ks[4 * w], v[w].y ^ ks[4 * w + 1],
-                                              v[w].z ^ ks[4 * w + 2], v[w].w ^ ks[4 * w + 3]), nb);
-        if (POLY && !DECRYPT) poly_block(p, o.x, o.y, o.z, o.w);
-        if (nb == 16) store16<true>(dst + off + 16 * w, o, 16);
-        else store16<false>(dst + off + 16 * w, o, nb);
-      }
-    }
-    if (POLY) {
-      R.ptail[0] = p.h0; R.ptail[1] = p.h1; R.ptail[2] = p.h2; R.ptail[3] = p.h3;
-      R.ptail[4] = p.h4;
     }
   }
 }
@@ -992,21 +915,42 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   RecHdr *hdr_w = const_cast<RecHdr *>(hdr);
 #define NOISE_DESC_BIG(ST)                                                     \
   NOISE_DESC_TILE(9, 16384, ST)                                                \
+  NOISE_DESC_MTILE(9, 16384, ST)                                               \
   NOISE_DESC_TILE(8, 8192, ST)                                                 \
+  NOISE_DESC_MTILE(8, 8192, ST)                                                \
   NOISE_DESC_TILE(7, 4096, ST)                                                 \
-  NOISE_DESC_TILE(6, 2048, ST)
+  NOISE_DESC_MTILE(7, 4096, ST)                                                \
+  NOISE_DESC_TILE(6, 2048, ST)                                                 \
+  NOISE_DESC_MTILE(6, 2048, ST)
 #define NOISE_DESC_TILES()                                                     \
   NOISE_DESC_TILE(0, 64, ax.aux)                                               \
+  NOISE_DESC_MTILE(0, 64, ax.aux)                                              \
   NOISE_DESC_TILE(1, 128, ax.aux)                                              \
+  NOISE_DESC_MTILE(1, 128, ax.aux)                                             \
   NOISE_DESC_TILE(2, 192, ax.aux)                                              \
+  NOISE_DESC_MTILE(2, 192, ax.aux)                                             \
   NOISE_DESC_TILE(3, 256, ax.aux)                                              \
+  NOISE_DESC_MTILE(3, 256, ax.aux)                                             \
   NOISE_DESC_TILE(4, 512, ax.aux)                                              \
+  NOISE_DESC_MTILE(4, 512, ax.aux)                                             \
   NOISE_DESC_TILE(5, 1024, ax.aux)                                             \
+  NOISE_DESC_MTILE(5, 1024, ax.aux)                                            \
   hipLaunchKernelGGL((k_aead_records<DECRYPT>), gg, dim3(kGenBlock), 0, ax.aux, keys, nkeys, recs,  \
                      nrec, idx, hdr, in, out, ad, status);
 #define NOISE_DESC_TILE(C, LEN, ST)                                            \
   a.cls = C;                                                                   \
   hipLaunchKernelGGL((k_aead_tile<DECRYPT, LEN, false, kTileDesc>), grid, bt, 0, ST, a);
+  // the ragged records of the same capacity (the masked kernel)
+#define NOISE_DESC_MTILE(C, LEN, ST)                                           \
+  a.cls = kMCls0 + C;                                                          \
+  hipLaunchKernelGGL((k_aead_mtile<DECRYPT, LEN, kMTDesc>), grid, bt, 0, ST, a);
+  // the long records' tails (len % 1024 bytes) as masked 1 KiB tile units
+  TileArgs at = a;
+  at.tails = tails;
+  at.ntails = &hdr->counts[kColTails];
+  at.nlong = &hdr->nlong;
+  at.tail_split = nullptr;
+  at.chunk = -1;
   // the whole-record classes (2 .. 16 KiB) on a companion of their own, from
   // the fork: they are a quarter of config 4's bytes and would otherwise
   // queue behind (or ahead of) the small classes and the tails
@@ -1020,7 +964,7 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
     // then overlap the segment kernel's drain; tails first: -3..5 %)
     NOISE_DESC_TILES()
     if ((e = hipStreamWaitEvent(ax.aux, ax.prep, 0)) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_seg_tail<DECRYPT, kTailFused>), grid, bt, 0, ax.aux, tails, rt, hdr, in, out, -1);
+    hipLaunchKernelGGL((k_aead_mtile<false, 1024, kMTTail>), grid, bt, 0, ax.aux, at);
     if ((e = hipEventRecord(ax.join, ax.aux)) != hipSuccess) return e;
     // caller: every full segment of every long record, then the tags
     hipLaunchKernelGGL((k_aead_tile<DECRYPT, 1024, false, kTileSeg>), gseg, bt, 0, stream, a);
@@ -1033,7 +977,7 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   // decrypt.  Companion: the tails' Poly1305 first (the first tag check
   // waits for it), then the small classes and the generic kernel
   if ((e = hipStreamWaitEvent(ax.aux, ax.prep, 0)) != hipSuccess) return e;
-  hipLaunchKernelGGL((k_seg_tail<true, kTailPoly>), grid, bt, 0, ax.aux, tails, rt, hdr, in, out, -1);
+  hipLaunchKernelGGL((k_aead_mtile<true, 1024, kMTTailPoly>), grid, bt, 0, ax.aux, at);
   if ((e = hipEventRecord(ax.join, ax.aux)) != hipSuccess) return e;
   NOISE_DESC_TILES()
   // caller: per chunk, the Poly1305 pass and the tag check (the first one
@@ -1062,10 +1006,13 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
     hipLaunchKernelGGL((k_aead_tile<true, 1024, false, kTileSegXor, 0, 1, NOISE_XOR_SPAN>), gxor, bt, 0,
                        ax.aux2, ac);
     if ((e = hipStreamWaitEvent(ax.aux, ax.fin[c], 0)) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_seg_tail<true, kTailXor>), grid, bt, 0, ax.aux, tails, rt, hdr, in, out,
-                       cidx(c));
+    TileArgs atc = at;
+    atc.chunk = cidx(c);
+    atc.tail_split = chunks > 1 ? hdr->tsplit : nullptr;
+    hipLaunchKernelGGL((k_aead_mtile<true, 1024, kMTTailXor>), grid, bt, 0, ax.aux, atc);
   }
 #undef NOISE_DESC_TILE
+#undef NOISE_DESC_MTILE
 #undef NOISE_DESC_TILES
 #undef NOISE_DESC_BIG
   if ((e = hipEventRecord(ax.xdone, ax.aux2)) != hipSuccess) return e;

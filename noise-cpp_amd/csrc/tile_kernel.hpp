@@ -163,6 +163,12 @@ struct TileArgs {
   SegPartial *partial;           // kTileSeg: P_s words 0..3
   uint32_t *partial_hi;          // kTileSeg: P_s word 4
   const unsigned long long *nseg;  // kTileSeg: number of segments (device)
+  // the masked kernel (mtile_kernel.hpp)
+  uint32_t len;                         // kMTUniform: every record's length
+  const uint32_t *tails;                // kMTTail*: long records with a tail (SegRec index)
+  const unsigned long long *ntails;     // kMTTail*: their count (device)
+  const unsigned long long *tail_split; // kMTTail*: chunk boundaries in tails (device), or null
+  const unsigned long long *nlong;      // kMTTail*: long records in the scratch (device)
 };
 
 // kTileDesc: the class's slice of the sorted index array; kTileSeg: all

@@ -31,6 +31,10 @@ RECORDS_CASES = [
     ("cfg4", 2500, 8, 0),   # >= 1000 records (emulation build): the chunked decrypt pipeline
     ("inplace", 500, 5, (2 << 30) + 4096),
     ("ragged", 300, 6, 0),
+    # round 6: config-4 buckets minus U(0..63) -- the masked tile classes and
+    # the masked tail units of the long records, copy and in place
+    ("jitter", 700, 4, 0),
+    ("jitterinplace", 500, 5, 0),
 ]
 TRANSPORT_CASES = [
     ["pipeline", "10", "300", "2"],                       # launcher thread, tiny slots
@@ -59,6 +63,8 @@ def _job_list():
         jobs["records-%s-%d" % (mode, nrec)] = (
             [BIN, mode, str(nrec), str(seed), str(gap)], ASAN_NOLEAK, 900)
     jobs["records-overflow"] = ([BIN + "_seg300ull", "cfg4", "700", "7", "0"], ASAN_NOLEAK, 900)
+    # the uniform entry off the exact tile table: the masked tile kernel
+    jobs["uniform"] = ([os.path.join(BUILD, "emu_uniform"), "5"], ASAN_NOLEAK, 900)
     # leak detection on: noise_gpu_ctx_destroy and noise_gpu_thread_release
     # must free everything the engine allocated (the run ends with both)
     jobs["api"] = ([os.path.join(BUILD, "emu_api")], "detect_leaks=1", 1500)
@@ -78,6 +84,7 @@ def emu():
     _make("GRID_CAP=3u")
     _make("GRID_CAP=3u", "SEG_CAP=300ull")
     _make("GRID_CAP=3u", "api")
+    _make("GRID_CAP=3u", "uniform")
     _make("GRID_CAP=3u", "transport")
     _make("handshake")
     jobs = _job_list()
@@ -125,6 +132,20 @@ def test_records_path_emulated(emu, mode, nrec, seed, gap):
     assert "ok (0 failures)" in r.stdout
     assert ": 0 stores of unverified plaintext" in r.stdout
     assert "watched 0 failed" not in r.stdout  # the batch holds tampered long records
+
+
+def test_uniform_ragged_lengths_emulated(emu):
+    """noise_gpu_{en,de}crypt_uniform at 33 lengths off the exact tile table
+    (1 .. 16383, every class edge), 16-byte aligned strides, copy and in
+    place: the masked tile kernel (csrc/mtile_kernel.hpp) bit-exact against
+    the oracle under AddressSanitizer, no store outside a record's output
+    (ct || tag / plaintext), and -- with tampered tags, first and last
+    ciphertext bytes -- no store of unverified plaintext (monocypher.c:
+    2912-2929)."""
+    r = _result(emu, "uniform")
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]
+    assert "0 stores outside, 0 stores of unverified plaintext" in r.stdout
+    assert "ok (0 failures)" in r.stdout
 
 
 def test_host_entry_points_emulated_and_wiped(emu):

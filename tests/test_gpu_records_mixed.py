@@ -419,3 +419,90 @@ def test_whole_record_classes_tamper(oracle, in_place):
             assert st[i] == noise_amd.REC_OK, (i, L, st[i])
             assert back[o:o + L] == pts[i], (i, L)
         assert back[o + L:o + L + 16] == b"\x3c" * 16, ("wrote past the record", i, L)
+
+
+RAGGED = [1, 33, 64, 65, 100, 127, 129, 191, 193, 255, 257, 300, 480, 511, 513, 700, 961, 1000, 1023, 1025,
+          1040, 1400, 1985, 2047, 2049, 3000, 4033, 4095, 4097, 5000, 8129, 8191, 8193, 9000, 16000, 16321,
+          16383, 16385, 17000, 32705, 32767, 65456, 65500, 65519]
+
+
+@pytest.mark.parametrize("in_place", [False, True], ids=["copy", "in_place"])
+def test_ragged_classes_tamper(oracle, in_place):
+    """Round 6: records of every length class OFF
+    the exact tile table -- 1 .. 16383 B take the masked tile classes
+    (mtile_kernel.hpp: a record whole in one wave's tile, its tag checked
+    there before any plaintext is stored), 16385 .. 65519 B the 1 KiB
+    segments with a masked tail unit -- beside exact records in one batch.
+    Encrypt bit-exact against the oracle, nothing written past a record's
+    ct || tag; then every 5th record tampered (first / last ciphertext byte
+    or a tag byte) and decrypted: REC_BAD_MAC, a failed copy zeroed, a
+    failed in-place record untouched, nothing written past a record."""
+    rng = random.Random(0x52414747 + in_place)
+    nkeys = 7
+    keys = [rng.randbytes(32) for _ in range(nkeys)]
+    recs = []
+    for L in RAGGED * 50 + TILE * 10:  # > 2048 records: the classified path
+        recs.append([L, b"", rng.randrange(nkeys), rng.getrandbits(64) % (2**64 - 2), 0, 0])
+    rng.shuffle(recs)
+    pts = [rng.randbytes(r[0]) for r in recs]
+    d_keys = dev(b"".join(keys))
+    # encrypt (copy layout; the in-place variant encrypts in place too)
+    desc, din, dout, _ = layout(recs, decrypt=False, in_place=in_place)
+    src = bytearray(din)
+    fill(src, desc, pts, "in_off")
+    if in_place:
+        d_buf = dev(src)
+        noise_amd.encrypt_records(d_keys, nkeys, dev(desc.view(np.uint8)), len(recs), d_buf, d_buf, dev(b""))
+        ct_img = host(d_buf)
+    else:
+        d_out = torch.full((dout,), 0x3C, dtype=torch.uint8, device="cuda")
+        noise_amd.encrypt_records(d_keys, nkeys, dev(desc.view(np.uint8)), len(recs), dev(src), d_out, dev(b""))
+        ct_img = host(d_out)
+    cts = []
+    for i, (L, _, ki, n, _, _) in enumerate(recs):
+        o = int(desc[i]["out_off"])
+        want = oracle.encrypt(keys[ki], n, b"", pts[i])
+        assert ct_img[o:o + L + 16] == want, ("encrypt", i, L)
+        if not in_place:
+            assert ct_img[o + L + 16:o + L + 32] == b"\x3c" * 16, ("wrote past the record", i, L)
+        cts.append(bytearray(want))
+    bad = set(range(2, len(recs), 5))
+    for i in bad:
+        L = recs[i][0]
+        pos = [0, L - 1, L + rng.randrange(16)][i % 3]
+        cts[i][pos] ^= 1 << rng.randrange(8)
+    d_st = torch.full((len(recs),), 9, dtype=torch.uint8, device="cuda")
+    if in_place:
+        ddesc, nbytes, _, _ = layout(recs, decrypt=True, in_place=True)
+        buf = bytearray(nbytes)
+        fill(buf, ddesc, cts, "in_off")
+        d_buf = dev(buf)
+        noise_amd.decrypt_records(d_keys, nkeys, dev(ddesc.view(np.uint8)), len(recs), d_buf, d_buf, d_st,
+                                  dev(b""))
+        res, st = host(d_buf), host(d_st)
+        for i, (L, _, _, _, _, _) in enumerate(recs):
+            o = int(ddesc[i]["in_off"])
+            if i in bad:
+                assert st[i] == noise_amd.REC_BAD_MAC, (i, L)
+                assert res[o:o + L + 16] == bytes(cts[i]), ("in-place failure must keep ct", i, L)
+            else:
+                assert st[i] == noise_amd.REC_OK, (i, L, st[i])
+                assert res[o:o + L] == pts[i], (i, L)
+                assert res[o + L:o + L + 16] == bytes(cts[i][L:]), ("in-place decrypt wrote the tag", i, L)
+        return
+    ddesc, din, dout, _ = layout(recs, decrypt=True)
+    cin = bytearray(din)
+    fill(cin, ddesc, cts, "in_off")
+    d_back = torch.full((dout,), 0x3C, dtype=torch.uint8, device="cuda")
+    noise_amd.decrypt_records(d_keys, nkeys, dev(ddesc.view(np.uint8)), len(recs), dev(cin), d_back, d_st,
+                              dev(b""))
+    back, st = host(d_back), host(d_st)
+    for i, (L, _, _, _, _, _) in enumerate(recs):
+        o = int(ddesc[i]["out_off"])
+        if i in bad:
+            assert st[i] == noise_amd.REC_BAD_MAC, (i, L)
+            assert back[o:o + L] == bytes(L), ("failed copy must be zeroed", i, L)
+        else:
+            assert st[i] == noise_amd.REC_OK, (i, L, st[i])
+            assert back[o:o + L] == pts[i], (i, L)
+        assert back[o + L:o + L + 16] == b"\x3c" * 16, ("wrote past the record", i, L)

@@ -96,7 +96,7 @@ def run_one(torch, stream, layout, L, mib, reps):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mib", type=int, default=512, help="plaintext per length (MiB)")
+    ap.add_argument("--mib", type=int, default=2048, help="plaintext per length (MiB)")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--layouts", default="uniform-aligned,uniform-packed,records")
     ap.add_argument("lengths", nargs="*", type=int)

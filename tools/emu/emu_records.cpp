@@ -10,6 +10,8 @@
 //                   out-of-place encrypt + decrypt + tamper
 //     mode inplace: same lengths, encrypt and decrypt in place
 //     mode ragged : lengths uniform in 1..70000 (odd tails, > 65535 generic)
+//     mode jitter : config-4 buckets minus U(0..63) bytes (the masked tile
+//                   classes and masked tail units); jitterinplace: in place
 //   emu_records <mode> <nrec> <seed> <gap>: records start <gap> bytes into
 //     each buffer (e.g. 4 GiB, to exercise 64-bit offsets)
 // Test infrastructure only (links oracle/chachapoly_oracle.c).
@@ -88,8 +90,10 @@ int main(int argc, char **argv) {
   const char *mode = argc > 1 ? argv[1] : "cfg4";
   const uint64_t R = argc > 2 ? std::strtoull(argv[2], nullptr, 0) : 3000;
   const uint64_t seed = argc > 3 ? std::strtoull(argv[3], nullptr, 0) : 4;
-  const bool in_place = std::strcmp(mode, "inplace") == 0;
+  const bool in_place = std::strcmp(mode, "inplace") == 0 || std::strcmp(mode, "jitterinplace") == 0;
   const bool ragged = std::strcmp(mode, "ragged") == 0;
+  // jitter: config-4 buckets, each length lowered by U(0..63) (bench.py --jitter)
+  const bool jitter = std::strcmp(mode, "jitter") == 0 || std::strcmp(mode, "jitterinplace") == 0;
   const uint64_t gap = argc > 4 ? std::strtoull(argv[4], nullptr, 0) : 0;
 
   double w[11], tot = 0;
@@ -104,6 +108,7 @@ int main(int argc, char **argv) {
       if (u < c) break;
     }
     lens[i] = k == 10 ? 65519u : (64u << k);
+    if (jitter) lens[i] = std::min(65519u, (64u << k) - (uint32_t)(mix64(seed * 3 + i) % 64u));
     if (ragged) lens[i] = 1u + (uint32_t)(mix64(seed * 7 + i) % 70000u);  // long tails, > 65535
   }
   std::vector<noise_gpu_record> enc(R), dec(R);

@@ -277,6 +277,8 @@ inline int dpp_ror(int v, int ctrl) {
 #define __builtin_amdgcn_wave_barrier() (emu::ctx.wave->bar.arrive_and_wait())
 #define __builtin_amdgcn_alignbit(hi, lo, s)                                     \
   ((uint32_t)((((uint64_t)(uint32_t)(hi) << 32) | (uint32_t)(lo)) >> ((s) & 31)))
+#define __builtin_amdgcn_alignbyte(hi, lo, s)                                    \
+  ((uint32_t)((((uint64_t)(uint32_t)(hi) << 32) | (uint32_t)(lo)) >> (8 * ((s) & 3))))
 // LDS-DMA: lane l copies 16 bytes to lds_base + 16*l
 #define __builtin_amdgcn_global_load_lds(g, l, sz, off, aux)                     \
   std::memcpy((char *)(void *)(l) + 16 * emu::ctx.lane, (const void *)(g), 16)

@@ -373,12 +373,13 @@ typedef __attribute__((address_space(1))) u32x4 g_u32x4;
 typedef __attribute__((address_space(3))) void lds_void;
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
-// The record DMAs stream (NT = true, the nt policy: each byte is read once).
-// Same box, six alternating runs each (round 4, profiles/round4/ab/dma_nt.md):
-// config 2 +0.0..+2.3 %, config 4 +0.9..+2.6 %, every run faster; "sc1 nt"
-// and "sc0 sc1 nt" were no better.  NT = false (default policy) is for data
-// that is read again soon after (tile_load's POLICY).
-__device__ __forceinline__ void lds_dma16_s_nt(const void *sbase, uint32_t voff, lds_void *lds_base) {
+// The record DMAs stream (the nt policy: each byte is read once).  Same box,
+// six alternating runs each (round 4, profiles/round4/ab/dma_nt.md): config 2
+// +0.0..+2.3 %, config 4 +0.9..+2.6 %, every run faster; "sc1 nt" and
+// "sc0 sc1 nt" were no better, and the default policy on the decrypt's
+// Poly1305 pass (whose ciphertext the keystream pass reads again) was no
+// faster at 4..64 chunks (round 5, profiles/round5/ab/cfg4_chunks_policy.txt).
+__device__ __forceinline__ void lds_dma16_s(const void *sbase, uint32_t voff, lds_void *lds_base) {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(NOISE_DMA_BUILTIN)
   asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 nt"
                :: "v"(voff), "s"(sbase), "s"((uint32_t)(uintptr_t)lds_base) : "memory", "m0");
@@ -386,40 +387,13 @@ __device__ __forceinline__ void lds_dma16_s_nt(const void *sbase, uint32_t voff,
   __builtin_amdgcn_global_load_lds((const void *)((const uint8_t *)sbase + voff), lds_base, 16, 0, 0);
 #endif
 }
-__device__ __forceinline__ void lds_dma16_s_rt(const void *sbase, uint32_t voff, lds_void *lds_base) {
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(NOISE_DMA_BUILTIN)
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
-               :: "v"(voff), "s"(sbase), "s"((uint32_t)(uintptr_t)lds_base) : "memory", "m0");
-#else
-  __builtin_amdgcn_global_load_lds((const void *)((const uint8_t *)sbase + voff), lds_base, 16, 0, 0);
-#endif
-}
-__device__ __forceinline__ void lds_dma16_v_nt(const void *vaddr, lds_void *lds_base) {
+__device__ __forceinline__ void lds_dma16_v(const void *vaddr, lds_void *lds_base) {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(NOISE_DMA_BUILTIN)
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt"
                :: "v"(vaddr), "s"((uint32_t)(uintptr_t)lds_base) : "memory", "m0");
 #else
   __builtin_amdgcn_global_load_lds(vaddr, lds_base, 16, 0, 0);
 #endif
-}
-__device__ __forceinline__ void lds_dma16_v_rt(const void *vaddr, lds_void *lds_base) {
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(NOISE_DMA_BUILTIN)
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
-               :: "v"(vaddr), "s"((uint32_t)(uintptr_t)lds_base) : "memory", "m0");
-#else
-  __builtin_amdgcn_global_load_lds(vaddr, lds_base, 16, 0, 0);
-#endif
-}
-// NT = true: streaming (nt) policy; false: the default (data read again soon)
-template <bool NT = true>
-__device__ __forceinline__ void lds_dma16_s(const void *sbase, uint32_t voff, lds_void *lds_base) {
-  if constexpr (NT) lds_dma16_s_nt(sbase, voff, lds_base);
-  else lds_dma16_s_rt(sbase, voff, lds_base);
-}
-template <bool NT = true>
-__device__ __forceinline__ void lds_dma16_v(const void *vaddr, lds_void *lds_base) {
-  if constexpr (NT) lds_dma16_v_nt(vaddr, lds_base);
-  else lds_dma16_v_rt(vaddr, lds_base);
 }
 // The same with system-scope cache bypass (sc0 sc1): for host-mapped memory
 // that the host rewrites while a resident kernel keeps running (no kernel

@@ -96,13 +96,23 @@ __host__ __device__ constexpr uint32_t req_inline_chunks(uint32_t ad_len, uint32
 // The check is per lane, folded into the seq compare (round 5): round 4's
 // single check word needed a cross-lane sum on the accept path.  The chunk
 // constant keeps an all-zero image (never a request) from decoding to one
-// seq in all four header chunks.
+// seq in all four header chunks.  The tag is non-linear (round 6, ADVICE
+// r5): the words are multiplied by odd constants before they are combined
+// and the sum goes through a multiply / xorshift finaliser, so a tear that
+// leaves stale (e.g. wiped, zero) payload words under a new seq word does
+// not decode to that seq for structured payloads the way XOR-of-rotations
+// did (len 64 with nonce 2^26 cancelled exactly: rotl(64, 7) == rotl(2^26,
+// 19)).  tests/cpp/req_tag_test.cpp tears chunk 0 over small meta / nonces.
 __host__ __device__ constexpr uint32_t req_rotl(uint32_t x, int n) {
   return (x << n) | (x >> (32 - n));
 }
 __host__ __device__ constexpr uint32_t req_chunk_tag(uint32_t chunk, uint32_t w1, uint32_t w2,
                                                      uint32_t w3) {
-  return req_rotl(w1, 7) ^ req_rotl(w2, 19) ^ w3 ^ (0x9e3779b9u * (chunk + 1u));
+  uint32_t x = w1 * 0x9e3779b1u + (chunk + 1u) * 0x7f4a7c15u;
+  x ^= req_rotl(w2 * 0x85ebca6bu, 13);
+  x ^= req_rotl(w3 * 0xc2b2ae35u, 17);
+  x *= 0x27d4eb2fu;
+  return x ^ (x >> 15);
 }
 __host__ __device__ constexpr OneLayout one_layout(uint32_t ad_len, uint32_t len) {
   const uint64_t a16 = (ad_len + 15ull) & ~15ull, l16 = (len + 15ull) & ~15ull;

@@ -8,31 +8,24 @@
 //
 // Layout: the record's bytes sit in the tile at their own (16-byte aligned)
 // positions, as for an exact record; only the lanes' view is shifted.  A
-// class of capacity L has CV = L / 64 ChaCha chunk slots and PV = L / 16
-// Poly1305 block slots per record, G lanes of CPL chunks / BPL blocks each.
-// A record of C = ceil(len / 64) chunks and P = ceil(len / 16) blocks is
-// RIGHT-aligned in that virtual space:
-//   virtual chunk v  <-> real chunk  v - (CV - C)   (absent when negative)
-//   virtual block v  <-> real block  v - (PV - P)   (absent when negative)
-// so the absent slots are LEADING ones.  A leading absent Poly1305 block reads
-// the tile's zero slot with no 2^128 bit: Horner from h = 0 stays 0 through
-// it, so every lane's partial sum keeps the exact-size weight r^(BPL (G-1-j))
-// and the recombination is tile_kernel.hpp's, unchanged -- no per-record
-// powers.  The real chunk count and block count differ by t = 4C - P in
-// [0, 3] blocks, so a lane's Poly1305 span can start up to 3 blocks into the
-// previous virtual chunk -- the previous lane's last one for j > 0:
-//   encrypt: the lanes first XOR their LAST virtual chunk (into the tile),
-//     then chunks 0, 1, ... with the Poly1305 of chunk k right after the XOR
-//     of chunk k (ChaCha of chunk k + 1 interleaved with it);
-//   decrypt: Poly1305 of chunk k over the ciphertext, the XOR of chunk k - 1
-//     after it (so no ciphertext is overwritten before it is MACed).
-// The last real block's bytes past len are zeroed in the tile before it is
-// MACed (encrypt: the ciphertext tail; decrypt: the tag bytes, after the tag
-// was read out), as the AEAD's zero padding.  The tag sits at byte len: it is
-// read out of (decrypt) / shifted into (encrypt) the two 16-byte pieces it
-// straddles.  Stores: the whole 16-byte pieces of the output, then the
-// partial last piece byte-wise -- no byte past the record's output is
-// written (len + 16 encrypt, len decrypt; Noise wire ct || tag).
+// class of capacity L has CV = L / 64 ChaCha chunk slots per record, G lanes
+// of CPL chunks each.  A record of C = ceil(len / 64) chunks is RIGHT-aligned
+// in them: lane j's virtual chunk v is real chunk CPL j + v - (CV - C), absent
+// when negative -- the absent chunks are LEADING ones.  The MAC of a lane
+// starts from h = 0, so resetting h to 0 after each absent chunk makes them
+// vanish, and every lane keeps the exact-size weight r^(BPL (G-1-j)): the
+// recombination is tile_kernel.hpp's, unchanged, with no per-record powers.
+// The loop is tile_kernel.hpp's too: one LDS read of a piece feeds the XOR
+// and the MAC, and the ChaCha block of chunk k + 1 is computed beside the
+// XOR / MAC of chunk k.  Only the record's last chunk (lane G-1's last) is
+// special: its MAC input is masked to the record's bytes (the AEAD's zero
+// padding: no tag bytes, keystream or stale tile bytes), and its blocks past
+// P = ceil(len / 16) multiply by r = 1 with no 2^128 bit -- identities.
+// The tag sits at byte len: it is read out of (decrypt) / shifted into
+// (encrypt) the two 16-byte pieces it straddles.  Stores: the whole 16-byte
+// pieces of the output, then the partial last piece (dword / short / byte
+// stores) -- no byte past the record's output is written (len + 16 encrypt,
+// len decrypt; Noise wire ct || tag).
 //
 // Reads: the 16-byte aligned pieces holding the record's input bytes are
 // read whole.  A record starts 16-byte aligned (the callers check it), so the
@@ -69,17 +62,22 @@ namespace noise_amd {
 
 enum MTileMode : int { kMTUniform = 0, kMTDesc = 1, kMTTail = 2, kMTTailPoly = 3, kMTTailXor = 4 };
 
-// 16 bytes at byte offset k (1..15) of the 32-byte little-endian [lo | hi]
+// 16 bytes at byte offset k (1..15) of the 32-byte little-endian [lo | hi].
+// The word shift by k / 4 (0..3) is two v_perm word selects per word (a
+// plain select of w[i + 2] / w[i] is turned into a scratch-indexed load by
+// the compiler), then a byte funnel (v_alignbyte).
+__device__ __forceinline__ uint32_t wsel(uint32_t sel, uint32_t a, uint32_t b) {
+  return __builtin_amdgcn_perm(a, b, sel);  // sel 0x07060504: a, 0x03020100: b
+}
 __device__ __forceinline__ uint4 extract16(const uint4 lo, const uint4 hi, uint32_t k) {
-  uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-  // word shift by k / 4 (0..3) in two select stages, then a byte funnel
-  const bool s8 = (k & 8u) != 0, s4 = (k & 4u) != 0;
+  const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  const uint32_t s8 = (k & 8u) ? 0x07060504u : 0x03020100u, s4 = (k & 4u) ? 0x07060504u : 0x03020100u;
   uint32_t u[6];
 #pragma unroll
-  for (int i = 0; i < 6; ++i) u[i] = s8 ? w[i + 2] : w[i];
+  for (int i = 0; i < 6; ++i) u[i] = wsel(s8, w[i + 2], w[i]);
   uint32_t v[5];
 #pragma unroll
-  for (int i = 0; i < 5; ++i) v[i] = s4 ? u[i + 1] : u[i];
+  for (int i = 0; i < 5; ++i) v[i] = wsel(s4, u[i + 1], u[i]);
   const uint32_t b = k & 3u;
   uint4 o;
   o.x = __builtin_amdgcn_alignbyte(v[1], v[0], b);
@@ -89,21 +87,23 @@ __device__ __forceinline__ uint4 extract16(const uint4 lo, const uint4 hi, uint3
   return o;
 }
 
-// Poly1305 block with a selectable 2^128 bit: hb = 0 and m = 0 on h = 0 is
-// the identity (a leading absent block); hb = 1 is poly_block
-__device__ __forceinline__ void poly_block_hb(Poly1305 &p, uint32_t m0, uint32_t m1, uint32_t m2,
-                                              uint32_t m3, uint32_t hb) {
+// Poly1305 block with explicit r values: (r = 1, rr = 0, r0lo = 1, hb = 0,
+// m = 0) leaves h unchanged (partially reduced) -- a trailing absent block
+__device__ __forceinline__ void poly_block_r(Poly1305 &p, uint32_t m0, uint32_t m1, uint32_t m2,
+                                             uint32_t m3, uint32_t hb, uint32_t r0, uint32_t r1,
+                                             uint32_t r2, uint32_t r3, uint32_t rr0, uint32_t rr1,
+                                             uint32_t rr2, uint32_t rr3, uint32_t r0lo) {
   unsigned c;
   const uint32_t s0 = __builtin_addc(p.h0, m0, 0u, &c);
   const uint32_t s1 = __builtin_addc(p.h1, m1, c, &c);
   const uint32_t s2 = __builtin_addc(p.h2, m2, c, &c);
   const uint32_t s3 = __builtin_addc(p.h3, m3, c, &c);
   const uint32_t s4 = p.h4 + c + hb;
-  const uint64_t x0 = mad64(s0, p.r0, mad64(s1, p.rr3, mad64(s2, p.rr2, mad64(s3, p.rr1, mad64(s4, p.rr0, 0)))));
-  const uint64_t x1 = mad64(s0, p.r1, mad64(s1, p.r0, mad64(s2, p.rr3, mad64(s3, p.rr2, mad64(s4, p.rr1, 0)))));
-  const uint64_t x2 = mad64(s0, p.r2, mad64(s1, p.r1, mad64(s2, p.r0, mad64(s3, p.rr3, mad64(s4, p.rr2, 0)))));
-  const uint64_t x3 = mad64(s0, p.r3, mad64(s1, p.r2, mad64(s2, p.r1, mad64(s3, p.r0, mad64(s4, p.rr3, 0)))));
-  const uint32_t x4 = __umul24(s4, p.r0lo);
+  const uint64_t x0 = mad64(s0, r0, mad64(s1, rr3, mad64(s2, rr2, mad64(s3, rr1, mad64(s4, rr0, 0)))));
+  const uint64_t x1 = mad64(s0, r1, mad64(s1, r0, mad64(s2, rr3, mad64(s3, rr2, mad64(s4, rr1, 0)))));
+  const uint64_t x2 = mad64(s0, r2, mad64(s1, r1, mad64(s2, r0, mad64(s3, rr3, mad64(s4, rr2, 0)))));
+  const uint64_t x3 = mad64(s0, r3, mad64(s1, r2, mad64(s2, r1, mad64(s3, r0, mad64(s4, rr3, 0)))));
+  const uint32_t x4 = __umul24(s4, r0lo);
   const uint32_t u5 = x4 + (uint32_t)(x3 >> 32);
   const uint32_t q = u5 >> 2;
   p.h0 = __builtin_addc(q + (q << 2), (uint32_t)x0, 0u, &c);
@@ -116,7 +116,22 @@ __device__ __forceinline__ void poly_block_hb(Poly1305 &p, uint32_t m0, uint32_t
 // The first `n` (1..15) bytes of a 16-byte piece at a 16-byte aligned
 // address: whole dwords, then a short and a byte as needed
 __device__ __forceinline__ void store_head(uint8_t *p, uint4 v, uint32_t n) {
-  store16<false>(p, v, (int)n);
+#if defined(NOISE_HIP_EMU)
+  store16<false>(p, v, (int)n);  // the emulator's store hook sees it as one store
+#else
+  typedef __attribute__((address_space(1))) uint32_t g_u32;
+  typedef __attribute__((address_space(1))) uint16_t g_u16;
+  typedef __attribute__((address_space(1))) uint8_t g_u8;
+  g_u32 *p32 = (g_u32 *)p;
+  if (n >= 4u) p32[0] = v.x;
+  if (n >= 8u) p32[1] = v.y;
+  if (n >= 12u) p32[2] = v.z;
+  const uint32_t q = n >> 2, rem = n & 3u;
+  const uint32_t last = q == 0u ? v.x : q == 1u ? v.y : q == 2u ? v.z : v.w;
+  uint8_t *t = p + 4u * q;
+  if (rem & 2u) *(g_u16 *)t = (uint16_t)last;
+  if (rem & 1u) *(g_u8 *)(t + (rem & 2u)) = (uint8_t)(last >> (8u * (rem & 2u)));
+#endif
 }
 
 template <bool DECRYPT, int L, int MODE>
@@ -148,6 +163,18 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
   const uint32_t lane = threadIdx.x;
   const uint32_t rho = lane / G, j = lane % G;
   if (lane == 0) lds[ZSLOT] = make_uint4(0u, 0u, 0u, 0u);  // never overwritten
+  // mtab[n]: the mask keeping the first n (0..16) bytes of a 16-byte piece
+  __shared__ uint4 mtab[17];
+  if (lane <= 16u) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int b = (int)lane - 4 * i;
+      w[i] = b >= 4 ? 0xffffffffu : b <= 0 ? 0u : (1u << (8 * b)) - 1u;
+    }
+    mtab[lane] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  wave_lds_fence();
   uint32_t gl[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) gl[i] = swz<256>(64u * i + lane) - 64u * i;
@@ -182,6 +209,9 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
     uint32_t own_in_lo = 0, own_in_hi = 0, own_out_lo = 0, own_out_hi = 0;
     bool own_bad = false, own_inplace = false, own_ok = true;
     uint32_t kr[4] = {0u, 0u, 0u, 0u}, kss[4] = {0u, 0u, 0u, 0u};
+    F26 own_rt;  // r^(16 - t) (G > 1; from the SegRec for the tails)
+#pragma unroll
+    for (int i = 0; i < 5; ++i) own_rt.a[i] = 0u;
     F26 pw[C::LOG2G > 0 ? C::LOG2G : 1];
 #pragma unroll
     for (int b = 0; b < (C::LOG2G > 0 ? C::LOG2G : 1); ++b)
@@ -224,12 +254,14 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
             if (DO_POLY) {
 #pragma unroll
               for (int i = 0; i < 4; ++i) kr[i] = R.r[i];
-              // G = 4 lanes: r^16, r^32 (k_seg_prep)
+              // G = 4 lanes: r^16, r^32, and r^(16 - t) of the tail (k_seg_prep)
 #pragma unroll
               for (int b = 0; b < C::LOG2G; ++b) {
                 pw[b].a[0] = R.pwlo[b][0]; pw[b].a[1] = R.pwlo[b][1];
                 pw[b].a[2] = R.pwlo[b][2]; pw[b].a[3] = R.pwlo[b][3]; pw[b].a[4] = R.pwhi[b];
               }
+#pragma unroll
+              for (int i = 0; i < 5; ++i) own_rt.a[i] = R.r16t[i];
             }
           } else {
             own_len = 0;  // beyond the segment scratch: the generic kernel has it
@@ -258,9 +290,39 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
       }
     }
     // input pieces of the record (decrypt: ct || tag, encrypt: pt / a tail)
-    const uint32_t own_np = TAG_IN ? (own_len + 31u) >> 4 : (own_len + 15u) >> 4;
+    // t = 4 C - P: Poly1305 blocks the record's last ChaCha chunk lacks
+    const uint32_t own_t = 4u * ((own_len + 63u) >> 6) - ((own_len + 15u) >> 4);
 
     // the first tile's DMA goes out before the key block and lands meanwhile
+    // a record's length and offsets by its key lane kl: computed in the
+    // uniform mode (record super0 + kl: no cross-lane traffic), read from the
+    // key lane otherwise -- *_s for a wave-uniform kl (v_readlane into SGPRs),
+    // *_v for a per-lane kl (ds_bpermute)
+    constexpr uint32_t TAGB = TAG_IN ? 31u : 15u;  // input pieces: (len + TAGB) >> 4
+    auto len_s = [&](uint32_t kl) -> uint32_t {
+      return MODE == kMTUniform ? a.len : (uint32_t)__builtin_amdgcn_readlane((int)own_len, (int)kl);
+    };
+    auto len_v = [&](uint32_t kl) -> uint32_t {
+      return MODE == kMTUniform ? a.len : (uint32_t)__shfl((int)own_len, (int)kl);
+    };
+    auto in_s = [&](uint32_t kl) -> uint64_t {
+      if (MODE == kMTUniform) return (super0 + kl) * a.in_stride;
+      return join64((uint32_t)__builtin_amdgcn_readlane((int)own_in_hi, (int)kl),
+                    (uint32_t)__builtin_amdgcn_readlane((int)own_in_lo, (int)kl));
+    };
+    auto in_v = [&](uint32_t kl) -> uint64_t {
+      if (MODE == kMTUniform) return (super0 + kl) * a.in_stride;
+      return join64((uint32_t)__shfl((int)own_in_hi, (int)kl), (uint32_t)__shfl((int)own_in_lo, (int)kl));
+    };
+    auto out_s = [&](uint32_t kl) -> uint64_t {
+      if (MODE == kMTUniform) return (super0 + kl) * a.out_stride;
+      return join64((uint32_t)__builtin_amdgcn_readlane((int)own_out_hi, (int)kl),
+                    (uint32_t)__builtin_amdgcn_readlane((int)own_out_lo, (int)kl));
+    };
+    auto out_v = [&](uint32_t kl) -> uint64_t {
+      if (MODE == kMTUniform) return (super0 + kl) * a.out_stride;
+      return join64((uint32_t)__shfl((int)own_out_hi, (int)kl), (uint32_t)__shfl((int)own_out_lo, (int)kl));
+    };
     auto load_tile = [&](uint64_t rec0, uint32_t t_rpt) {
       const uint64_t left = nrec - rec0;
       const uint32_t nv = left < (uint64_t)RPT ? (uint32_t)left : (uint32_t)RPT;
@@ -270,23 +332,21 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
 #pragma unroll
         for (int q = 0; q < REC_SLOTS / 64; ++q) {
           const uint32_t kl = t_rpt + (uint32_t)q / KPR;
-          const uint32_t np = (uint32_t)__builtin_amdgcn_readlane((int)own_np, (int)kl);
+          const uint32_t np = (len_s(kl) + TAGB) >> 4;
           const uint32_t kib = 64u * ((uint32_t)q % KPR);
           if ((uint32_t)(q / KPR) < nv && kib < np) {
-            const uint64_t off = join64((uint32_t)__builtin_amdgcn_readlane((int)own_in_hi, (int)kl),
-                                        (uint32_t)__builtin_amdgcn_readlane((int)own_in_lo, (int)kl)) +
-                                 1024ull * ((uint32_t)q % KPR);
+            const uint64_t off = in_s(kl) + 1024ull * ((uint32_t)q % KPR);
             const uint32_t pc = kib + glq<256>(gl, q);
-            if (pc < np) lds_dma16_s<true>(in + off, 16u * glq<256>(gl, q), (lds_void *)(NOISE_LDS3(lds) + 64 * q));
+            if (pc < np) lds_dma16_s(in + off, 16u * glq<256>(gl, q), (lds_void *)(NOISE_LDS3(lds) + 64 * q));
           }
         }
         if (TAG_IN) {  // piece SPR of record r (the tag of a full-size record) -> tag slot r
           const uint32_t r = lane < (uint32_t)RPT ? lane : 0u;
           const uint32_t src = t_rpt + r;
-          const uint64_t off = join64((uint32_t)__shfl((int)own_in_hi, (int)src), (uint32_t)__shfl((int)own_in_lo, (int)src));
-          const uint32_t np = (uint32_t)__shfl((int)own_np, (int)src);
+          const uint64_t off = in_v(src);
+          const uint32_t np = (len_v(src) + TAGB) >> 4;
           if (lane < (uint32_t)RPT && lane < nv && np > (uint32_t)SPR)
-            lds_dma16_v<true>(in + off + 16u * SPR, (lds_void *)(NOISE_LDS3(lds) + REC_SLOTS));
+            lds_dma16_v(in + off + 16u * SPR, (lds_void *)(NOISE_LDS3(lds) + REC_SLOTS));
         }
       } else {
 #pragma unroll
@@ -302,10 +362,10 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
             p = SPR;
           }
           const uint32_t src = t_rpt + (r < (uint32_t)RPT ? r : 0u);
-          const uint64_t off = join64((uint32_t)__shfl((int)own_in_hi, (int)src), (uint32_t)__shfl((int)own_in_lo, (int)src));
-          const uint32_t np = (uint32_t)__shfl((int)own_np, (int)src);
+          const uint64_t off = in_v(src);
+          const uint32_t np = (len_v(src) + TAGB) >> 4;
           if (s < (uint32_t)IN_SLOTS && r < nv && p < np)
-            lds_dma16_v<true>(in + off + 16u * p, (lds_void *)(NOISE_LDS3(lds) + 64 * q));
+            lds_dma16_v(in + off + 16u * p, (lds_void *)(NOISE_LDS3(lds) + 64 * q));
         }
       }
     };
@@ -320,10 +380,22 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
       kr[3] = otk[3] & 0x0ffffffcu;
       kss[0] = otk[4]; kss[1] = otk[5]; kss[2] = otk[6]; kss[3] = otk[7];
       if (G > 1) {
+        static_assert(G == 1 || C::LOG2BPL == 4, "lanes of 16 Poly1305 blocks");
         F26 x = to26(kr[0], kr[1], kr[2], kr[3], 0u);
-#pragma unroll
-        for (int b = 0; b < C::LOG2BPL; ++b) x = mul26(x, x);
+        const F26 x1 = x;
+        const F26 x2 = mul26(x1, x1), x4 = mul26(x2, x2), x8 = mul26(x4, x4);
+        x = mul26(x8, x8);
         pw[0] = x;
+        // r^(16 - t): the weight of a full lane's sum past the lane before
+        // the record's last (module comment); t = 4 C - P blocks short
+        const uint32_t tt = own_t;
+        if (__ballot(tt != 0u)) {
+          const F26 one = to26(1u, 0u, 0u, 0u, 0u);
+          F26 y = mul26(x8, x4);                                // r^12
+          y = mul26(y, (tt == 1u || tt == 2u) ? x2 : one);      // r^14 (t <= 2)
+          own_rt = mul26(y, (tt == 1u || tt == 3u) ? x1 : one); // r^15 (t = 1), r^13 (t = 3)
+          if (tt == 0u) own_rt = x;
+        }
 #pragma unroll
         for (int b = 1; b < C::LOG2G; ++b) pw[b] = mul26(pw[b - 1], pw[b - 1]);
       }
@@ -339,10 +411,10 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
       const uint32_t src = (uint32_t)t * RPT + rho;  // key lane of my record
       const bool valid = rho < nv;
       // ---- this lane's record ------------------------------------------
-      const uint32_t rlen = (uint32_t)__shfl((int)own_len, (int)src);
+      const uint32_t rlen = len_v(src);
       const uint32_t P = (rlen + 15u) >> 4, Cc = (rlen + 63u) >> 6;
       const uint32_t F = rlen >> 4, sb = rlen & 15u;  // whole pieces, bytes in the last one
-      const int D = (int)(L / 16) - (int)P, dc = (int)(L / 64) - (int)Cc;
+      const int dc = (int)(L / 64) - (int)Cc;  // leading absent chunks
       const uint32_t rbase = rho * SPR;
       auto pslot = [&](uint32_t i) -> uint32_t {  // record piece i (0 .. SPR) -> slot
         return i < (uint32_t)SPR ? swz<256>(rbase + i) : (uint32_t)REC_SLOTS + rho;
@@ -379,114 +451,85 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
       }
       const bool bad_key = MODE == kMTDesc && __shfl((int)own_bad, (int)src) != 0;
 
-      // ---- decrypt: the tag out of the tile, zero padding for the MAC ----
+      // ---- decrypt: the tag out of the tile (bytes rlen .. rlen + 15) ------
       uint4 want = make_uint4(0u, 0u, 0u, 0u);
       if (TAG_IN) {
         const uint4 A = lb[pslot(F)];
         const uint4 B = lb[sb ? pslot(F + 1u) : (uint32_t)ZSLOT];
         want = sb ? extract16(A, B, sb) : A;
-        wave_lds_fence();
-        if (sb && j == 0 && valid) lb[pslot(F)] = mask_bytes(A, (int)sb);
-        wave_lds_fence();
-      } else if (POLY_PRE && DO_POLY) {  // tail Poly1305 pass: zero the bytes past the tail
-        const uint4 A = lb[pslot(F)];
-        wave_lds_fence();  // (wave-wide: no barrier inside lane-divergent code)
-        if (sb && j == 0 && valid) lb[pslot(F)] = mask_bytes(A, (int)sb);
-        wave_lds_fence();
       }
+      wave_lds_fence();  // the tag is read before lane G-1's XOR rewrites its first piece
 
-      // ---- ChaCha20 XOR and Poly1305, right-aligned (see the top) ------
-      const int rc0 = (int)(CPL * j) - dc;          // real chunk of my virtual chunk 0
-      const int rb0 = (int)(BPL * j) - D;           // real block of my virtual block 0
+      // ---- ChaCha20 XOR and Poly1305, right-aligned by whole chunks ------
+      // (the top of the file).  As in tile_kernel.hpp, ONE LDS read of a
+      // piece feeds both the XOR and the MAC, and the ChaCha block of chunk
+      // kk + 1 is computed beside the XOR / MAC of chunk kk.  Leading absent
+      // chunks: garbage in a junk slot, h reset to 0 after each of them.  The
+      // last chunk (lane G-1's, the record's last real one): the MAC input is
+      // masked to the record's bytes (zero padding), and its trailing absent
+      // blocks (past P) multiply by r = 1 with no 2^128 bit -- identities.
+      const int rc0 = (int)(CPL * j) - dc;  // real chunk of my virtual chunk 0
+      const uint32_t lbytes = j == (uint32_t)G - 1u ? rlen - 64u * (Cc - 1u) : 64u;  // bytes in my last chunk
+      const uint32_t lblk = (lbytes + 15u) >> 4;                                      // blocks in it (1..4)
       ChaPre pre{};
       if (DO_XOR) pre = chacha_pre(kt, n_lo, n_hi);
-      auto keystream = [&](int vc, uint32_t ks[16]) {
-        chacha20_block_pre(kt, cbase + (uint32_t)(rc0 + vc), pre, n_lo, n_hi, ks);
-      };
-      auto xor_chunk = [&](int vc, const uint32_t ks[16]) {
-        const int c = rc0 + vc;
+      uint32_t ks[16];
+      if (DO_XOR) chacha20_block_pre(kt, cbase + (uint32_t)rc0, pre, n_lo, n_hi, ks);
+#pragma unroll
+      for (int kk = 0; kk < CPL; ++kk) {
+        const int c = rc0 + kk;
+        uint32_t ksn[16];
+        if (DO_XOR && kk + 1 < CPL) chacha20_block_pre(kt, cbase + (uint32_t)(c + 1), pre, n_lo, n_hi, ksn);
+        const bool last = kk == CPL - 1;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const uint32_t slot = c >= 0 ? swz<256>(rbase + 4u * (uint32_t)c + (uint32_t)q) : (uint32_t)JSLOT;
           const uint4 v = lb[slot];
-          uint4 o;
-          o.x = v.x ^ ks[4 * q + 0];
-          o.y = v.y ^ ks[4 * q + 1];
-          o.z = v.z ^ ks[4 * q + 2];
-          o.w = v.w ^ ks[4 * q + 3];
-          lb[slot] = o;
-        }
-      };
-      auto poly_chunk = [&](int vc) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int b = rb0 + 4 * vc + q;
-          const uint32_t slot = b >= 0 ? swz<256>(rbase + (uint32_t)b) : (uint32_t)ZSLOT;
-          const uint4 v = lb[slot];
-          poly_block_hb(p, v.x, v.y, v.z, v.w, b >= 0 ? 1u : 0u);
-        }
-      };
-      if (!DO_XOR) {  // tail Poly1305 pass
-#pragma unroll
-        for (int kk = 0; kk < CPL; ++kk) poly_chunk(kk);
-      } else if (!DO_POLY) {  // tail plaintext pass
-        uint32_t ks[16];
-        keystream(0, ks);
-#pragma unroll
-        for (int kk = 0; kk < CPL; ++kk) {
-          uint32_t ksn[16];
-          if (kk + 1 < CPL) keystream(kk + 1, ksn);
-          xor_chunk(kk, ks);
-          if (kk + 1 < CPL) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) ks[i] = ksn[i];
+          uint4 o = v;
+          if (DO_XOR) {
+            o.x = v.x ^ ks[4 * q + 0];
+            o.y = v.y ^ ks[4 * q + 1];
+            o.z = v.z ^ ks[4 * q + 2];
+            o.w = v.w ^ ks[4 * q + 3];
+            lb[slot] = o;
+          }
+          if (DO_POLY) {
+            uint4 m = POLY_PRE ? v : o;
+            if (last) {
+              // the record's last chunk: bytes past rlen (tag bytes, stale
+              // pieces, keystream) must not reach the MAC
+              const int nb = (int)lbytes - 16 * q;
+              const uint4 mk = mtab[nb <= 0 ? 0 : (nb >= 16 ? 16 : nb)];
+              m.x &= mk.x; m.y &= mk.y; m.z &= mk.z; m.w &= mk.w;
+            }
+            if (last && q > 0) {  // a trailing absent block is the identity (r = 1, no 2^128)
+              const bool on = (uint32_t)q < lblk;
+              poly_block_r(p, m.x, m.y, m.z, m.w, on ? 1u : 0u, on ? p.r0 : 1u, on ? p.r1 : 0u,
+                           on ? p.r2 : 0u, on ? p.r3 : 0u, on ? p.rr0 : 0u, on ? p.rr1 : 0u,
+                           on ? p.rr2 : 0u, on ? p.rr3 : 0u, on ? p.r0lo : 1u);
+            } else {
+              poly_block(p, m.x, m.y, m.z, m.w);
+            }
           }
         }
-      } else if (POLY_PRE) {
-        // decrypt: Poly1305 of chunk kk over the ciphertext, then the XOR of
-        // chunk kk - 1 (chunk kk's MAC may reach 3 blocks into chunk kk - 1)
-        uint32_t ksp[16];
-#pragma unroll
-        for (int kk = 0; kk < CPL; ++kk) {
-          uint32_t ksc[16];
-          keystream(kk, ksc);
-          poly_chunk(kk);
-          if (kk > 0) xor_chunk(kk - 1, ksp);
-#pragma unroll
-          for (int i = 0; i < 16; ++i) ksp[i] = ksc[i];
+        if (DO_POLY && c < 0) {  // a leading absent chunk: start the Horner chain over
+          p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0u;
         }
-        wave_lds_fence();  // every lane's last MAC read (the next lane's chunk 0) before this write
-        xor_chunk(CPL - 1, ksp);
-      } else {
-        // encrypt: the last chunk first (the next lane's first MAC blocks
-        // may lie in it), its tail bytes zeroed; then chunk kk, its MAC
-        {
-          uint32_t ksl[16];
-          keystream(CPL - 1, ksl);
-          xor_chunk(CPL - 1, ksl);
-        }
-        wave_lds_fence();
-        if (sb && j == (uint32_t)G - 1u && valid) lb[pslot(F)] = mask_bytes(lb[pslot(F)], (int)sb);
-        wave_lds_fence();
-        uint32_t ks[16];
-        if (CPL > 1) keystream(0, ks);
+        if (DO_XOR && kk + 1 < CPL) {
 #pragma unroll
-        for (int kk = 0; kk < CPL; ++kk) {
-          uint32_t ksn[16];
-          if (kk + 1 < CPL - 1) keystream(kk + 1, ksn);
-          if (kk < CPL - 1) xor_chunk(kk, ks);
-          poly_chunk(kk);
-          if (kk + 1 < CPL - 1) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) ks[i] = ksn[i];
-          }
+          for (int i = 0; i < 16; ++i) ks[i] = ksn[i];
         }
       }
 
       // ---- recombination: sum_j acc_j r^(BPL (G-1-j)) (tile_kernel.hpp) --
       if (DO_POLY && G > 1) {
+        // lane j's sum is followed by BPL (G-1-j) - t real blocks: weight
+        // r^(BPL (G-2-j)) r^(16 - t) for j < G-1, 1 for the last lane (t = 0
+        // in the whole tile: the exact-size weights r^(BPL (G-1-j)))
         F26 h = to26(p.h0, p.h1, p.h2, p.h3, p.h4);
-        const uint32_t m = (uint32_t)G - 1u - j;
+        const uint32_t rt_t = 4u * Cc - P;
+        const bool any_t = __ballot(valid && rt_t != 0u) != 0;
+        const uint32_t m = any_t ? (j + 1u < (uint32_t)G ? (uint32_t)G - 2u - j : 0u) : (uint32_t)G - 1u - j;
 #pragma unroll
         for (int b = 0; b < C::LOG2G; ++b) {
           F26 f;
@@ -494,6 +537,16 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
 #pragma unroll
           for (int i = 0; i < 5; ++i) {
             const uint32_t w = __shfl(pw[b].a[i], src);
+            f.a[i] = use ? w : (i == 0 ? 1u : 0u);
+          }
+          h = mul26(h, f);
+        }
+        if (any_t) {  // wave-uniform
+          F26 f;
+          const bool use = j + 1u < (uint32_t)G;
+#pragma unroll
+          for (int i = 0; i < 5; ++i) {
+            const uint32_t w = __shfl(own_rt.a[i], src);
             f.a[i] = use ? w : (i == 0 ? 1u : 0u);
           }
           h = mul26(h, f);
@@ -547,7 +600,7 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
           lb[pslot(F)] = T;
         } else {
           const uint4 Z = make_uint4(0u, 0u, 0u, 0u);
-          const uint4 A = lb[pslot(F)];  // ciphertext, zero past rlen
+          const uint4 A = mask_bytes(lb[pslot(F)], (int)sb);  // ciphertext bytes before rlen
           const uint4 lo = extract16(Z, T, 16u - sb), hi = extract16(T, Z, 16u - sb);
           lb[pslot(F)] = make_uint4(A.x | lo.x, A.y | lo.y, A.z | lo.z, A.w | lo.w);
           lb[pslot(F + 1u)] = hi;
@@ -568,95 +621,100 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
       // whole pieces go out as 16-byte stores, in NPART parts (fewer pieces
       // live in registers); the next tile's DMA overwrites the tile, so it
       // is issued after the last part's gather, before that part's stores.
+      // Only the gathered pieces live across the DMA: each store's record,
+      // guard and address are worked out after it.
       constexpr int NOUT = WHOLE_KIB ? (REC_SLOTS / 64 + (TAG_OUT ? 1 : 0)) : (RPT * OPR + 63) / 64;
       constexpr int NPART = NOUT > 8 ? 2 : 1;
       constexpr int NQ = (NOUT + NPART - 1) / NPART;
       const bool full = nv == (uint32_t)RPT;
+      // output piece q of this lane: its record r, piece index pc, tile slot
+      auto piece = [&](int q, uint32_t &r, uint32_t &pc, uint32_t &slot, bool &ok) {
+        if (WHOLE_KIB && q < REC_SLOTS / 64) {  // KiB q % KPR of record q / KPR
+          r = (uint32_t)q / KPR;
+          pc = 64u * ((uint32_t)q % KPR) + lane;
+          slot = swz<256>(64u * q + lane);
+          ok = true;
+        } else if (WHOLE_KIB) {  // the tag slots (piece SPR), lane r -> record r
+          r = lane < (uint32_t)RPT ? lane : 0u;
+          pc = SPR;
+          slot = REC_SLOTS + r;
+          ok = lane < (uint32_t)RPT;
+        } else {
+          const uint32_t g = 64u * q + lane;
+          r = g / OPR;
+          pc = g % OPR;
+          ok = (RPT * OPR) % 64 == 0 || g < (uint32_t)(RPT * OPR);
+          if (!ok) r = 0;
+          slot = pc < (uint32_t)SPR ? swz<256>(r * SPR + pc) : (uint32_t)REC_SLOTS + r;
+        }
+      };
+      const uint32_t pr = lane < (uint32_t)RPT ? lane : 0u;  // the partial piece's record
 #pragma unroll
       for (int part = 0; part < NPART; ++part) {
         uint4 ov[NQ];
-        bool st[NQ];
-        uint64_t dst[NQ];
 #pragma unroll
         for (int qq = 0; qq < NQ; ++qq) {
           const int q = part * NQ + qq;
-          st[qq] = false;
-          dst[qq] = 0;
           ov[qq] = make_uint4(0u, 0u, 0u, 0u);
           if (q >= NOUT) break;
           uint32_t r, pc, slot;
           bool ok;
-          if (WHOLE_KIB && q < REC_SLOTS / 64) {  // KiB q % KPR of record q / KPR
-            r = (uint32_t)q / KPR;
-            pc = 64u * ((uint32_t)q % KPR) + lane;
-            slot = swz<256>(64u * q + lane);
-            ok = true;
-          } else if (WHOLE_KIB) {  // the tag slots (piece SPR), lane r -> record r
-            r = lane < (uint32_t)RPT ? lane : 0u;
-            pc = SPR;
-            slot = REC_SLOTS + r;
-            ok = lane < (uint32_t)RPT;
-          } else {
-            const uint32_t g = 64u * q + lane;
-            r = g / OPR;
-            pc = g % OPR;
-            ok = (RPT * OPR) % 64 == 0 || g < (uint32_t)(RPT * OPR);
-            if (!ok) r = 0;
-            slot = pc < (uint32_t)SPR ? swz<256>(r * SPR + pc) : (uint32_t)REC_SLOTS + r;
-          }
-          const uint32_t kl = (uint32_t)t * RPT + r;
-          uint32_t ln, olo, ohi;
-          if (WHOLE_KIB && q < REC_SLOTS / 64) {  // one record per instruction: wave-uniform
-            ln = (uint32_t)__builtin_amdgcn_readlane((int)own_len, (int)kl);
-            olo = (uint32_t)__builtin_amdgcn_readlane((int)own_out_lo, (int)kl);
-            ohi = (uint32_t)__builtin_amdgcn_readlane((int)own_out_hi, (int)kl);
-          } else {
-            ln = (uint32_t)__shfl((int)own_len, (int)kl);
-            olo = (uint32_t)__shfl((int)own_out_lo, (int)kl);
-            ohi = (uint32_t)__shfl((int)own_out_hi, (int)kl);
-          }
-          const uint32_t nfo = (ln + (TAG_OUT ? 16u : 0u)) >> 4;  // whole output pieces
-          st[qq] = ok && (full || r < nv) && pc < nfo;
-          dst[qq] = join64(ohi, olo) + 16ull * pc;
+          piece(q, r, pc, slot, ok);
           ov[qq] = lb[slot];
-          if ((fail_mask >> (r * G)) & 1u) {  // not output as computed (rare)
-            const bool bk = ((badk_mask >> (r * G)) & 1u) != 0;
-            const bool inpl = ((inpl_mask >> (r * G)) & 1u) != 0;
-            st[qq] = st[qq] && DECRYPT && !inpl && !bk;
-            ov[qq] = make_uint4(0u, 0u, 0u, 0u);
-          }
         }
         // the partial last piece of record `lane` (read before the DMA)
         uint4 pv = make_uint4(0u, 0u, 0u, 0u);
-        uint32_t pn = 0u;
-        uint64_t pdst = 0;
         if (part == NPART - 1) {
-          const uint32_t r = lane < (uint32_t)RPT ? lane : 0u;
-          const uint32_t kl = (uint32_t)t * RPT + r;
-          const uint32_t ln = (uint32_t)__shfl((int)own_len, (int)kl);
-          const uint32_t olo = (uint32_t)__shfl((int)own_out_lo, (int)kl);
-          const uint32_t ohi = (uint32_t)__shfl((int)own_out_hi, (int)kl);
-          const uint32_t ob = ln + (TAG_OUT ? 16u : 0u);
+          const uint32_t ob = len_v((uint32_t)t * RPT + pr) + (TAG_OUT ? 16u : 0u);
           const uint32_t pp = ob >> 4;  // its piece index
-          pn = ob & 15u;
-          const uint32_t slot = pp < (uint32_t)SPR ? swz<256>(r * SPR + pp) : (uint32_t)REC_SLOTS + r;
-          pv = lb[pn ? slot : (uint32_t)ZSLOT];
-          if (!(lane < (uint32_t)RPT && lane < nv)) pn = 0u;
-          if ((fail_mask >> (r * G)) & 1u) {
-            const bool bk = ((badk_mask >> (r * G)) & 1u) != 0;
-            const bool inpl = ((inpl_mask >> (r * G)) & 1u) != 0;
-            if (!DECRYPT || inpl || bk) pn = 0u;
-            pv = make_uint4(0u, 0u, 0u, 0u);
-          }
-          pdst = join64(ohi, olo) + 16ull * pp;
+          const uint32_t slot = pp < (uint32_t)SPR ? swz<256>(pr * SPR + pp) : (uint32_t)REC_SLOTS + pr;
+          pv = lb[(ob & 15u) ? slot : (uint32_t)ZSLOT];
           wait_lds();  // every LDS read of this tile done
           wave_lds_fence();
           if (t + 1 < NTS && rec0 + RPT < nrec) load_tile(rec0 + RPT, (uint32_t)(t + 1) * RPT);
         }
 #pragma unroll
-        for (int qq = 0; qq < NQ; ++qq)
-          if (st[qq]) store16<true>(out + dst[qq], ov[qq], 16);
-        if (pn) store_head(out + pdst, pv, pn);
+        for (int qq = 0; qq < NQ; ++qq) {
+          const int q = part * NQ + qq;
+          if (q >= NOUT) break;
+          uint32_t r, pc, slot;
+          bool ok;
+          piece(q, r, pc, slot, ok);
+          const uint32_t kl = (uint32_t)t * RPT + r;
+          uint32_t ln;
+          uint64_t ob;
+          if (WHOLE_KIB && q < REC_SLOTS / 64) {  // one record per instruction: wave-uniform
+            ln = len_s(kl);
+            ob = out_s(kl);
+          } else {
+            ln = len_v(kl);
+            ob = out_v(kl);
+          }
+          const uint32_t nfo = (ln + (TAG_OUT ? 16u : 0u)) >> 4;  // whole output pieces
+          bool st = ok && (full || r < nv) && pc < nfo;
+          uint4 v = ov[qq];
+          if ((fail_mask >> (r * G)) & 1u) {  // not output as computed (rare)
+            const bool bk = ((badk_mask >> (r * G)) & 1u) != 0;
+            const bool inpl = ((inpl_mask >> (r * G)) & 1u) != 0;
+            st = st && DECRYPT && !inpl && !bk;
+            v = make_uint4(0u, 0u, 0u, 0u);
+          }
+          if (st) store16<true>(out + ob + 16ull * pc, v, 16);
+        }
+        if (part == NPART - 1) {
+          const uint32_t kl = (uint32_t)t * RPT + pr;
+          const uint32_t ob = len_v(kl) + (TAG_OUT ? 16u : 0u);
+          const uint64_t obase = out_v(kl);
+          uint32_t pn = ob & 15u;
+          if (!(lane < (uint32_t)RPT && lane < nv)) pn = 0u;
+          if ((fail_mask >> (pr * G)) & 1u) {
+            const bool bk = ((badk_mask >> (pr * G)) & 1u) != 0;
+            const bool inpl = ((inpl_mask >> (pr * G)) & 1u) != 0;
+            if (!DECRYPT || inpl || bk) pn = 0u;
+            pv = make_uint4(0u, 0u, 0u, 0u);
+          }
+          if (pn) store_head(out + obase + 16ull * (ob >> 4), pv, pn);
+        }
       }
     }
   }

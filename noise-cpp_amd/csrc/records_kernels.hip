@@ -463,13 +463,22 @@ __global__ __launch_bounds__(64) void k_seg_prep(const uint8_t *__restrict__ key
     // squaring chain r^(2^b); r^(tail blocks) = product over the bits of
     // the tail's Poly1305 block count (1..64)
     const uint32_t nbt = ((R.len & 1023u) + 15u) >> 4;
-    F26 x = to26(r0, r1, r2, r3, 0u), rt_pow;
+    F26 x = to26(r0, r1, r2, r3, 0u), rt_pow, xb[4];
     rt_pow.a[0] = 1u;
     rt_pow.a[1] = rt_pow.a[2] = rt_pow.a[3] = rt_pow.a[4] = 0u;
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
+      xb[b] = x;  // r^(2^b)
       if ((nbt >> b) & 1u) rt_pow = mul26(rt_pow, x);
       x = mul26(x, x);
+    }
+    {  // r^(16 - t) for the tail's masked tile unit (t = 4 ceil(tail / 64) - nbt)
+      const uint32_t t = 4u * (((R.len & 1023u) + 63u) >> 6) - nbt;
+      F26 y = t ? mul26(xb[3], xb[2]) : x;       // r^12 (r^16 when t = 0)
+      if (t == 1u || t == 2u) y = mul26(y, xb[1]);
+      if (t == 1u || t == 3u) y = mul26(y, xb[0]);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) R.r16t[i] = y.a[i];
     }
     // x = r^16
     if ((nbt >> 4) & 1u) rt_pow = mul26(rt_pow, x);
@@ -814,14 +823,32 @@ static hipError_t aux_get(AuxStream *out, hipStream_t stream) {
       return hipSuccess;
     }
   AuxStream a;
-  if ((e = hipStreamCreateWithFlags(&a.aux, hipStreamNonBlocking)) != hipSuccess) return e;
-  if ((e = hipStreamCreateWithFlags(&a.aux2, hipStreamNonBlocking)) != hipSuccess) return e;
-  if ((e = hipStreamCreateWithFlags(&a.aux3, hipStreamNonBlocking)) != hipSuccess) return e;
+  // on any failure, what was created so far is destroyed again
+  auto undo = [&a]() {
+    for (hipStream_t st : {a.aux, a.aux2, a.aux3})
+      if (st) (void)hipStreamDestroy(st);
+    for (hipEvent_t ev : {a.fork, a.prep, a.join, a.join2, a.xdone, a.big})
+      if (ev) (void)hipEventDestroy(ev);
+    for (int c = 0; c < kSegChunks; ++c)
+      for (hipEvent_t ev : {a.poly[c], a.fin[c]})
+        if (ev) (void)hipEventDestroy(ev);
+  };
+  for (hipStream_t *st : {&a.aux, &a.aux2, &a.aux3})
+    if ((e = hipStreamCreateWithFlags(st, hipStreamNonBlocking)) != hipSuccess) {
+      undo();
+      return e;
+    }
   for (hipEvent_t *ev : {&a.fork, &a.join, &a.prep, &a.join2, &a.xdone, &a.big})
-    if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return e;
+    if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) {
+      undo();
+      return e;
+    }
   for (int c = 0; c < kSegChunks; ++c)
     for (hipEvent_t *ev : {&a.poly[c], &a.fin[c]})
-      if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return e;
+      if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) {
+        undo();
+        return e;
+      }
   cache.push_back({dev, stream, a});
   *out = a;
   return hipSuccess;

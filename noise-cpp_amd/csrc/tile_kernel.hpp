@@ -127,7 +127,8 @@ struct SegRec {                  // one per long record, 256 B (two 128-B lines)
   uint32_t rtail[5];             // r^(tail blocks) (radix 2^26)
   uint32_t ptail[5];             // the tail's Poly1305 sum (radix 2^32, h4 small)
   uint32_t ok;                   // decrypt: 1 once the finalize kernel verified the tag
-  uint32_t pad[5];
+  uint32_t r16t[5];              // r^(16 - t) of the tail's masked tile unit (radix 2^26;
+                                 // t = 4 ceil(tail / 64) - ceil(tail / 16), mtile_kernel.hpp)
 };
 static_assert(sizeof(SegRec) == 256, "SegRec layout");
 struct SegEntry {                // one per full segment
@@ -200,11 +201,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
   using C = TileCfg<L, SPAN>;
   if (ABL == 1) return;
   constexpr bool TAGGED_IN = DECRYPT && MODE < kTileSeg;  // ct || tag pieces
-  // every record byte is read once: the streaming (nt) policy.  (Round 5:
-  // the default policy on the decrypt's Poly1305 pass, whose ciphertext the
-  // keystream pass reads again, was no faster at 4, 16, 32 or 64 chunks --
-  // profiles/round5/ab/cfg4_chunks_policy.txt.)
-  constexpr bool NT = true;
+  // every record byte is read once: the streaming (nt) policy (lds_dma16_*)
   constexpr int IN_SLOTS = TAGGED_IN ? C::NSLOT : C::REC_SLOTS;
   if (CONTIG) {
     // slot s = 64q + lane holds piece swz(s) = 64q + glq(gl, q); packed
@@ -219,7 +216,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
       for (int q = 0; q < C::REC_SLOTS / 64; ++q) {
         const uint32_t g = 64u * q + glq<SPAN>(gl, q);
         const uint32_t rr = g / C::SPR;
-        lds_dma16_s<NT>(base, DECRYPT ? 16u * (g + rr) : 16u * g, (lds_void *)(lds3 + 64 * q));
+        lds_dma16_s(base, DECRYPT ? 16u * (g + rr) : 16u * g, (lds_void *)(lds3 + 64 * q));
       }
     } else {
 #pragma unroll
@@ -227,7 +224,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
         const uint32_t g = 64u * q + glq<SPAN>(gl, q);
         const uint32_t rr = g / C::SPR;
         const uint32_t off = DECRYPT ? 16u * (g + rr) : 16u * g;
-        if (rr < nv) lds_dma16_s<NT>(base, off, (lds_void *)(lds3 + 64 * q));
+        if (rr < nv) lds_dma16_s(base, off, (lds_void *)(lds3 + 64 * q));
       }
     }
     if (TAGGED_IN) {  // tag pieces: slot REC_SLOTS + r <- piece (r, SPR)
@@ -235,7 +232,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
       for (int q = C::REC_SLOTS / 64; q < (C::NSLOT + 63) / 64; ++q) {
         const uint32_t r = 64u * q + lane - C::REC_SLOTS;
         if (r < nv)
-          lds_dma16_s<NT>(base, 16u * (r * (C::SPR + 1) + C::SPR), (lds_void *)(lds3 + 64 * q));
+          lds_dma16_s(base, 16u * (r * (C::SPR + 1) + C::SPR), (lds_void *)(lds3 + 64 * q));
       }
     }
   } else if (MODE >= kTileSeg || (MODE == kTileDesc && C::SPR % 64 == 0)) {
@@ -251,7 +248,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
         const uint64_t off = join64((uint32_t)__builtin_amdgcn_readlane((int)own_in_hi, (int)kl),
                                     (uint32_t)__builtin_amdgcn_readlane((int)own_in_lo, (int)kl)) +
                              1024ull * (q % KPR);
-        lds_dma16_s<NT>(in + off, 16u * glq<SPAN>(gl, q), (lds_void *)(lds3 + 64 * q));
+        lds_dma16_s(in + off, 16u * glq<SPAN>(gl, q), (lds_void *)(lds3 + 64 * q));
       }
     }
     if (TAGGED_IN) {  // decrypt: the RPT tags, lane r -> slot REC_SLOTS + r
@@ -259,7 +256,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
       const uint64_t off = ((uint64_t)(uint32_t)__shfl((int)own_in_hi, (int)(t_rpt + r)) << 32) |
                            (uint32_t)__shfl((int)own_in_lo, (int)(t_rpt + r));
       if (lane < (uint32_t)C::RPT && lane < nv)
-        lds_dma16_v<NT>(in + off + 16u * C::SPR, (lds_void *)(lds3 + C::REC_SLOTS));
+        lds_dma16_v(in + off + 16u * C::SPR, (lds_void *)(lds3 + C::REC_SLOTS));
     }
   } else {
 #pragma unroll 1
@@ -284,7 +281,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
         rec_base = in + (rec0 + r) * in_stride;
       }
       if (s < (uint32_t)IN_SLOTS && r < nv)
-        lds_dma16_v<NT>(rec_base + 16u * p, (lds_void *)(lds3 + 64 * q));
+        lds_dma16_v(rec_base + 16u * p, (lds_void *)(lds3 + 64 * q));
     }
   }
 }

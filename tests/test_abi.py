@@ -166,3 +166,18 @@ def test_reference_free_function_signatures(tmp_path):
         assert "no gfx950 device" in r.stdout
     else:
         assert r.returncode == 0 and "round trip ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_resident_request_tag_survives_tears(tmp_path):
+    """the resident request line's per-chunk check
+    (launchers.hpp req_chunk_tag) is non-linear -- a chunk torn into a new
+    seq word over stale (zero or previous) payload words does not decode to
+    the new seq for structured lengths / nonces (tests/cpp/req_tag_test.cpp,
+    host-only)."""
+    exe = str(tmp_path / "req_tag_test")
+    subprocess.run(["g++", "-std=c++20", "-O1", "-pthread", "-I", os.path.join(ROOT, "tools", "emu", "include"),
+                    "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "noise-cpp_amd", "csrc"),
+                    os.path.join(ROOT, "tests", "cpp", "req_tag_test.cpp"), "-o", exe], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "decode to the new seq" in r.stdout and ", 0 decode" in r.stdout

@@ -52,9 +52,18 @@ static std::atomic<const char *> phase{"start"};
 // each task of the process; the handler prints its own thread's stack with
 // the sanitizer's unwinder), once, so a stall names itself instead of
 // running into the test's time limit.
+// The handler is a last-resort diagnostic (it runs only after a 120-s stall;
+// the sanitizer's unwinder is not async-signal-safe).  SA_RESTART: the sleeps,
+// futex waits and barrier waits the signal interrupts in the emulated kernel
+// threads resume instead of returning early, so the run after a dump behaves
+// as the stalled run did.
 static void stack_handler(int) { __sanitizer_print_stack_trace(); }
 static void dump_all_stacks() {
-  signal(SIGUSR2, stack_handler);
+  struct sigaction sa {};
+  sa.sa_handler = stack_handler;
+  sigemptyset(&sa.sa_mask);
+  sa.sa_flags = SA_RESTART;
+  sigaction(SIGUSR2, &sa, nullptr);
   const pid_t me = (pid_t)syscall(SYS_gettid);
   if (DIR *d = opendir("/proc/self/task")) {
     while (dirent *e = readdir(d)) {

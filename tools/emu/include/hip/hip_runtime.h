@@ -279,6 +279,19 @@ inline int dpp_ror(int v, int ctrl) {
   ((uint32_t)((((uint64_t)(uint32_t)(hi) << 32) | (uint32_t)(lo)) >> ((s) & 31)))
 #define __builtin_amdgcn_alignbyte(hi, lo, s)                                    \
   ((uint32_t)((((uint64_t)(uint32_t)(hi) << 32) | (uint32_t)(lo)) >> (8 * ((s) & 3))))
+// v_perm_b32: byte i of the result = byte sel.byte[i] of {a (bytes 4..7), b (0..3)}
+// (selector bytes 0..7; 0x0c = 0x00, the only other value the kernels use)
+inline uint32_t emu_perm(uint32_t a, uint32_t b, uint32_t sel) {
+  const uint64_t x = ((uint64_t)a << 32) | b;
+  uint32_t r = 0;
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t sb = (sel >> (8 * i)) & 0xffu;
+    const uint32_t byte = sb < 8u ? (uint32_t)(x >> (8 * sb)) & 0xffu : 0u;
+    r |= byte << (8 * i);
+  }
+  return r;
+}
+#define __builtin_amdgcn_perm(a, b, s) emu_perm((uint32_t)(a), (uint32_t)(b), (uint32_t)(s))
 // LDS-DMA: lane l copies 16 bytes to lds_base + 16*l
 #define __builtin_amdgcn_global_load_lds(g, l, sz, off, aux)                     \
   std::memcpy((char *)(void *)(l) + 16 * emu::ctx.lane, (const void *)(g), 16)

@@ -47,6 +47,8 @@
 // The tail modes read r, r^16, r^32 and the key from the record's SegRec
 // (k_seg_prep) instead of a key pass; ChaCha counters continue at 1 + 16 nf.
 #pragma once
+#include <type_traits>
+
 #include "tile_kernel.hpp"
 
 namespace noise_amd {
@@ -153,6 +155,12 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
   constexpr int OPR = TAG_OUT ? SPR + 1 : SPR;  // output pieces of a full record
   constexpr int KPR = SPR / 64;                 // KiB per record (L >= 1024)
   constexpr bool WHOLE_KIB = SPR % 64 == 0;
+  // 256 / 512-byte classes: a DMA or store instruction covers RPI = 64 / SPR
+  // (4, 2) whole records -- their lengths and offsets come from RPI
+  // v_readlanes and a per-lane select instead of a shuffle per piece (the
+  // uniform mode computes them per lane: no shuffles to save)
+  constexpr bool SUB_KIB = KEYED && (SPR == 16 || SPR == 32);
+  constexpr int RPI = SUB_KIB ? 64 / SPR : 1;
   // records per super-tile: 64 (one key lane each), at most 128 KiB for
   // classes of 4 KiB and up (so that batches of large records make waves)
   constexpr int RPS = L > 2048 ? 64 * 2048 / L : 64;
@@ -182,8 +190,11 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
   // the work list
   uint64_t nrec = a.nrec, dbase = 0;
   if (MODE == kMTDesc) {
+    // the exact-size records of the capacity, then the ragged ones (adjacent
+    // in idx: k_cls_scatter); a super-tile of exact ones only takes the
+    // exact-size body below
     dbase = a.cls_base[a.cls];
-    nrec = a.counts[a.cls];
+    nrec = a.counts[a.cls] + (a.cls2 >= 0 ? a.counts[a.cls2] : 0ull);
   } else if (TAIL) {
     const uint64_t nall = *a.ntails;
     uint64_t lo = 0, hi = nall;
@@ -289,9 +300,14 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
         for (int i = 0; i < 8; ++i) own_k[i] = 0u;
       }
     }
-    // input pieces of the record (decrypt: ct || tag, encrypt: pt / a tail)
+    // the super-tile's body: EX = every record in it is exactly L bytes
+    // long (the exact-size records of a descriptor class come first in idx),
+    // the body then compiles to the exact-size kernel's -- no masks, no
+    // leading absent chunks, no r^(16 - t), whole-piece stores only
+    auto run = [&](auto ex_tag) {
+    constexpr bool EX = decltype(ex_tag)::value;
     // t = 4 C - P: Poly1305 blocks the record's last ChaCha chunk lacks
-    const uint32_t own_t = 4u * ((own_len + 63u) >> 6) - ((own_len + 15u) >> 4);
+    const uint32_t own_t = EX ? 0u : 4u * ((own_len + 63u) >> 6) - ((own_len + 15u) >> 4);
 
     // the first tile's DMA goes out before the key block and lands meanwhile
     // a record's length and offsets by its key lane kl: computed in the
@@ -300,9 +316,11 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
     // *_v for a per-lane kl (ds_bpermute)
     constexpr uint32_t TAGB = TAG_IN ? 31u : 15u;  // input pieces: (len + TAGB) >> 4
     auto len_s = [&](uint32_t kl) -> uint32_t {
+      if (EX) return (uint32_t)L;
       return MODE == kMTUniform ? a.len : (uint32_t)__builtin_amdgcn_readlane((int)own_len, (int)kl);
     };
     auto len_v = [&](uint32_t kl) -> uint32_t {
+      if (EX) return (uint32_t)L;
       return MODE == kMTUniform ? a.len : (uint32_t)__shfl((int)own_len, (int)kl);
     };
     auto in_s = [&](uint32_t kl) -> uint64_t {
@@ -322,6 +340,28 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
     auto out_v = [&](uint32_t kl) -> uint64_t {
       if (MODE == kMTUniform) return (super0 + kl) * a.out_stride;
       return join64((uint32_t)__shfl((int)own_out_hi, (int)kl), (uint32_t)__shfl((int)own_out_lo, (int)kl));
+    };
+    // record klb + sub (sub = 0 .. RPI-1 per lane): SUB_KIB classes
+    auto sel_q = [&](uint32_t own, uint32_t klb, uint32_t sub) -> uint32_t {
+      uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)own, (int)klb);
+#pragma unroll
+      for (int k = 1; k < RPI; ++k) {
+        const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)own, (int)(klb + k));
+        v = sub == (uint32_t)k ? w : v;
+      }
+      return v;
+    };
+    auto len_q = [&](uint32_t klb, uint32_t sub) -> uint32_t {
+      if (EX) return (uint32_t)L;
+      return MODE == kMTUniform ? a.len : sel_q(own_len, klb, sub);
+    };
+    auto in_q = [&](uint32_t klb, uint32_t sub) -> uint64_t {
+      if (MODE == kMTUniform) return (super0 + klb + sub) * a.in_stride;
+      return join64(sel_q(own_in_hi, klb, sub), sel_q(own_in_lo, klb, sub));
+    };
+    auto out_q = [&](uint32_t klb, uint32_t sub) -> uint64_t {
+      if (MODE == kMTUniform) return (super0 + klb + sub) * a.out_stride;
+      return join64(sel_q(own_out_hi, klb, sub), sel_q(own_out_lo, klb, sub));
     };
     auto load_tile = [&](uint64_t rec0, uint32_t t_rpt) {
       const uint64_t left = nrec - rec0;
@@ -348,8 +388,32 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
           if (lane < (uint32_t)RPT && lane < nv && np > (uint32_t)SPR)
             lds_dma16_v(in + off + 16u * SPR, (lds_void *)(NOISE_LDS3(lds) + REC_SLOTS));
         }
-      } else {
+      } else if constexpr (SUB_KIB) {
+        // instruction q: records q RPI .. q RPI + RPI-1; slot 64q + lane holds
+        // piece swz(64q + lane) = 64q + glq (swz stays inside 16-slot groups)
 #pragma unroll
+        for (int q = 0; q < REC_SLOTS / 64; ++q) {
+          const uint32_t gq = glq<256>(gl, q);
+          const uint32_t sub = gq / SPR, p = gq % SPR;
+          const uint32_t klb = t_rpt + (uint32_t)q * RPI;
+          const uint32_t np = (len_q(klb, sub) + TAGB) >> 4;
+          const uint64_t off = in_q(klb, sub);  // every lane reads (the emulator's readlane is collective)
+          if ((uint32_t)q * RPI + sub < nv && p < np)
+            lds_dma16_v(in + off + 16u * p, (lds_void *)(NOISE_LDS3(lds) + 64 * q));
+        }
+        if (TAG_IN) {  // as above
+          const uint32_t r = lane < (uint32_t)RPT ? lane : 0u;
+          const uint32_t src = t_rpt + r;
+          const uint64_t off = in_v(src);
+          const uint32_t np = (len_v(src) + TAGB) >> 4;
+          if (lane < (uint32_t)RPT && lane < nv && np > (uint32_t)SPR)
+            lds_dma16_v(in + off + 16u * SPR, (lds_void *)(NOISE_LDS3(lds) + REC_SLOTS));
+        }
+      } else {
+        // one DMA per iteration (as tile_kernel.hpp's): unrolled, every
+        // piece's shuffled address is live at once and the classes below
+        // 1 KiB spill
+#pragma unroll 1
         for (int q = 0; q < (IN_SLOTS + 63) / 64; ++q) {
           const uint32_t s = 64u * q + lane;
           uint32_t r, p;
@@ -389,7 +453,7 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
         // r^(16 - t): the weight of a full lane's sum past the lane before
         // the record's last (module comment); t = 4 C - P blocks short
         const uint32_t tt = own_t;
-        if (__ballot(tt != 0u)) {
+        if (!EX && __ballot(tt != 0u)) {
           const F26 one = to26(1u, 0u, 0u, 0u, 0u);
           F26 y = mul26(x8, x4);                                // r^12
           y = mul26(y, (tt == 1u || tt == 2u) ? x2 : one);      // r^14 (t <= 2)
@@ -483,7 +547,7 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
         const bool last = kk == CPL - 1;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const uint32_t slot = c >= 0 ? swz<256>(rbase + 4u * (uint32_t)c + (uint32_t)q) : (uint32_t)JSLOT;
+          const uint32_t slot = (EX || c >= 0) ? swz<256>(rbase + 4u * (uint32_t)c + (uint32_t)q) : (uint32_t)JSLOT;
           const uint4 v = lb[slot];
           uint4 o = v;
           if (DO_XOR) {
@@ -495,14 +559,14 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
           }
           if (DO_POLY) {
             uint4 m = POLY_PRE ? v : o;
-            if (last) {
+            if (!EX && last) {
               // the record's last chunk: bytes past rlen (tag bytes, stale
               // pieces, keystream) must not reach the MAC
               const int nb = (int)lbytes - 16 * q;
               const uint4 mk = mtab[nb <= 0 ? 0 : (nb >= 16 ? 16 : nb)];
               m.x &= mk.x; m.y &= mk.y; m.z &= mk.z; m.w &= mk.w;
             }
-            if (last && q > 0) {  // a trailing absent block is the identity (r = 1, no 2^128)
+            if (!EX && last && q > 0) {  // a trailing absent block is the identity (r = 1, no 2^128)
               const bool on = (uint32_t)q < lblk;
               poly_block_r(p, m.x, m.y, m.z, m.w, on ? 1u : 0u, on ? p.r0 : 1u, on ? p.r1 : 0u,
                            on ? p.r2 : 0u, on ? p.r3 : 0u, on ? p.rr0 : 0u, on ? p.rr1 : 0u,
@@ -512,7 +576,7 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
             }
           }
         }
-        if (DO_POLY && c < 0) {  // a leading absent chunk: start the Horner chain over
+        if (DO_POLY && !EX && c < 0) {  // a leading absent chunk: start the Horner chain over
           p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0u;
         }
         if (DO_XOR && kk + 1 < CPL) {
@@ -528,7 +592,7 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
         // in the whole tile: the exact-size weights r^(BPL (G-1-j)))
         F26 h = to26(p.h0, p.h1, p.h2, p.h3, p.h4);
         const uint32_t rt_t = 4u * Cc - P;
-        const bool any_t = __ballot(valid && rt_t != 0u) != 0;
+        const bool any_t = !EX && __ballot(valid && rt_t != 0u) != 0;
         const uint32_t m = any_t ? (j + 1u < (uint32_t)G ? (uint32_t)G - 2u - j : 0u) : (uint32_t)G - 1u - j;
 #pragma unroll
         for (int b = 0; b < C::LOG2G; ++b) {
@@ -623,8 +687,11 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
       // is issued after the last part's gather, before that part's stores.
       // Only the gathered pieces live across the DMA: each store's record,
       // guard and address are worked out after it.
-      constexpr int NOUT = WHOLE_KIB ? (REC_SLOTS / 64 + (TAG_OUT ? 1 : 0)) : (RPT * OPR + 63) / 64;
-      constexpr int NPART = NOUT > 8 ? 2 : 1;
+      constexpr bool REG = WHOLE_KIB || SUB_KIB;  // record pieces, then one instruction of tags
+      constexpr int NOUT = REG ? (REC_SLOTS / 64 + (TAG_OUT ? 1 : 0)) : (RPT * OPR + 63) / 64;
+      // (per-lane records below 1 KiB: every store shuffles its record's
+      // length and offset, so parts of <= 6 pieces -- more spill)
+      constexpr int NPART = REG ? (NOUT > 8 ? 2 : 1) : (NOUT + 5) / 6;
       constexpr int NQ = (NOUT + NPART - 1) / NPART;
       const bool full = nv == (uint32_t)RPT;
       // output piece q of this lane: its record r, piece index pc, tile slot
@@ -634,7 +701,12 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
           pc = 64u * ((uint32_t)q % KPR) + lane;
           slot = swz<256>(64u * q + lane);
           ok = true;
-        } else if (WHOLE_KIB) {  // the tag slots (piece SPR), lane r -> record r
+        } else if (SUB_KIB && q < REC_SLOTS / 64) {  // records q RPI + lane / SPR
+          r = (uint32_t)q * RPI + lane / SPR;
+          pc = lane % SPR;
+          slot = swz<256>(64u * q + lane);
+          ok = true;
+        } else if (REG) {  // the tag slots (piece SPR), lane r -> record r
           r = lane < (uint32_t)RPT ? lane : 0u;
           pc = SPR;
           slot = REC_SLOTS + r;
@@ -665,10 +737,12 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
         // the partial last piece of record `lane` (read before the DMA)
         uint4 pv = make_uint4(0u, 0u, 0u, 0u);
         if (part == NPART - 1) {
-          const uint32_t ob = len_v((uint32_t)t * RPT + pr) + (TAG_OUT ? 16u : 0u);
-          const uint32_t pp = ob >> 4;  // its piece index
-          const uint32_t slot = pp < (uint32_t)SPR ? swz<256>(pr * SPR + pp) : (uint32_t)REC_SLOTS + pr;
-          pv = lb[(ob & 15u) ? slot : (uint32_t)ZSLOT];
+          if (!EX) {
+            const uint32_t ob = len_v((uint32_t)t * RPT + pr) + (TAG_OUT ? 16u : 0u);
+            const uint32_t pp = ob >> 4;  // its piece index
+            const uint32_t slot = pp < (uint32_t)SPR ? swz<256>(pr * SPR + pp) : (uint32_t)REC_SLOTS + pr;
+            pv = lb[(ob & 15u) ? slot : (uint32_t)ZSLOT];
+          }
           wait_lds();  // every LDS read of this tile done
           wave_lds_fence();
           if (t + 1 < NTS && rec0 + RPT < nrec) load_tile(rec0 + RPT, (uint32_t)(t + 1) * RPT);
@@ -686,6 +760,10 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
           if (WHOLE_KIB && q < REC_SLOTS / 64) {  // one record per instruction: wave-uniform
             ln = len_s(kl);
             ob = out_s(kl);
+          } else if (SUB_KIB && q < REC_SLOTS / 64) {
+            const uint32_t klb = (uint32_t)t * RPT + (uint32_t)q * RPI;
+            ln = len_q(klb, lane / SPR);
+            ob = out_q(klb, lane / SPR);
           } else {
             ln = len_v(kl);
             ob = out_v(kl);
@@ -701,7 +779,7 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
           }
           if (st) store16<true>(out + ob + 16ull * pc, v, 16);
         }
-        if (part == NPART - 1) {
+        if (!EX && part == NPART - 1) {
           const uint32_t kl = (uint32_t)t * RPT + pr;
           const uint32_t ob = len_v(kl) + (TAG_OUT ? 16u : 0u);
           const uint64_t obase = out_v(kl);
@@ -716,6 +794,18 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
           if (pn) store_head(out + obase + 16ull * (ob >> 4), pv, pn);
         }
       }
+    }
+    };  // run
+    bool ex = false;
+    if (MODE == kMTDesc)
+      ex = __ballot(lane < (uint32_t)RPS && super0 + lane < nrec && own_len != (uint32_t)L) == 0;
+    if constexpr (MODE == kMTDesc) {
+      if (ex)
+        run(std::true_type{});
+      else
+        run(std::false_type{});
+    } else {
+      run(std::false_type{});
     }
   }
 }

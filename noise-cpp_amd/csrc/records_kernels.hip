@@ -29,6 +29,7 @@
 // Small batches (< kClassifyMin records) skip all this and run the generic
 // kernel directly (latency of single records from CipherState).
 // Scratch is a grow-only device buffer cached per (device, stream).
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -44,6 +45,12 @@ constexpr int kGenBlock = 256;
 constexpr int kNumTileCls = 10;           // exactly 64 128 192 256 512 1024 2048 4096 8192 16384
 constexpr int kMCls0 = kNumTileCls;       // the masked (ragged) classes: any other length up to
 constexpr int kNumMCls = 10;              //   the same ten capacities (mtile_kernel.hpp)
+static_assert(kNumMCls == kNumTileCls, "one ragged class per exact tile class");
+// idx order: exact class c, then the ragged class of the same capacity (one
+// masked-kernel launch takes both: launch_classes), then long and generic
+__host__ __device__ constexpr int cls_order(int k) {
+  return k < 2 * kNumTileCls ? ((k & 1) ? kMCls0 + k / 2 : k / 2) : k;
+}
 constexpr int kClsLong = kMCls0 + kNumMCls;  // segmented long records (> 16 KiB)
 constexpr int kClsGeneric = kClsLong + 1;
 constexpr int kNumCls = kClsLong + 2;
@@ -316,7 +323,8 @@ __global__ __launch_bounds__(64) void k_cls_scatter(
   {
     unsigned long long b = 0;
 #pragma unroll
-    for (int c = 0; c < kNumCls; ++c) {
+    for (int k = 0; k < kNumCls; ++k) {
+      const int c = cls_order(k);
       cbase[c] = b;
       b += hdr->counts[c];
     }
@@ -940,37 +948,43 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   const dim3 gxor(capped((segbound + 63) / 64, NOISE_GRID_CAP));
   const dim3 gfin(capped((nrec + 64 / NOISE_FIN_W - 1) / (64 / NOISE_FIN_W), NOISE_GRID_CAP));
   RecHdr *hdr_w = const_cast<RecHdr *>(hdr);
+  // one launch per capacity: the exact-size records of the class and the
+  // ragged ones of the same capacity (adjacent in idx, cls_order), the
+  // masked kernel switching to its exact-size body per super-tile.  Two
+  // launches per capacity (the exact tile kernel, then the masked one) left
+  // nearly empty launches queued between full ones: a capped grid of single
+  // -wave workgroups waits for CU slots even when it has no work (config-4
+  // traces, profiles/round6/ab).  NOISE_DESC_SPLIT=1 keeps the split form.
+#ifndef NOISE_DESC_SPLIT
+#define NOISE_DESC_SPLIT 0
+#endif
 #define NOISE_DESC_BIG(ST)                                                     \
-  NOISE_DESC_TILE(9, 16384, ST)                                                \
-  NOISE_DESC_MTILE(9, 16384, ST)                                               \
-  NOISE_DESC_TILE(8, 8192, ST)                                                 \
-  NOISE_DESC_MTILE(8, 8192, ST)                                                \
-  NOISE_DESC_TILE(7, 4096, ST)                                                 \
-  NOISE_DESC_MTILE(7, 4096, ST)                                                \
-  NOISE_DESC_TILE(6, 2048, ST)                                                 \
-  NOISE_DESC_MTILE(6, 2048, ST)
+  NOISE_DESC_CAP(9, 16384, ST)                                                 \
+  NOISE_DESC_CAP(8, 8192, ST)                                                  \
+  NOISE_DESC_CAP(7, 4096, ST)                                                  \
+  NOISE_DESC_CAP(6, 2048, ST)
 #define NOISE_DESC_TILES()                                                     \
-  NOISE_DESC_TILE(0, 64, ax.aux)                                               \
-  NOISE_DESC_MTILE(0, 64, ax.aux)                                              \
-  NOISE_DESC_TILE(1, 128, ax.aux)                                              \
-  NOISE_DESC_MTILE(1, 128, ax.aux)                                             \
-  NOISE_DESC_TILE(2, 192, ax.aux)                                              \
-  NOISE_DESC_MTILE(2, 192, ax.aux)                                             \
-  NOISE_DESC_TILE(3, 256, ax.aux)                                              \
-  NOISE_DESC_MTILE(3, 256, ax.aux)                                             \
-  NOISE_DESC_TILE(4, 512, ax.aux)                                              \
-  NOISE_DESC_MTILE(4, 512, ax.aux)                                             \
-  NOISE_DESC_TILE(5, 1024, ax.aux)                                             \
-  NOISE_DESC_MTILE(5, 1024, ax.aux)                                            \
+  NOISE_DESC_CAP(0, 64, ax.aux)                                                \
+  NOISE_DESC_CAP(1, 128, ax.aux)                                               \
+  NOISE_DESC_CAP(2, 192, ax.aux)                                               \
+  NOISE_DESC_CAP(3, 256, ax.aux)                                               \
+  NOISE_DESC_CAP(4, 512, ax.aux)                                               \
+  NOISE_DESC_CAP(5, 1024, ax.aux)                                              \
   hipLaunchKernelGGL((k_aead_records<DECRYPT>), gg, dim3(kGenBlock), 0, ax.aux, keys, nkeys, recs,  \
                      nrec, idx, hdr, in, out, ad, status);
-#define NOISE_DESC_TILE(C, LEN, ST)                                            \
+#if NOISE_DESC_SPLIT
+#define NOISE_DESC_CAP(C, LEN, ST)                                             \
   a.cls = C;                                                                   \
-  hipLaunchKernelGGL((k_aead_tile<DECRYPT, LEN, false, kTileDesc>), grid, bt, 0, ST, a);
-  // the ragged records of the same capacity (the masked kernel)
-#define NOISE_DESC_MTILE(C, LEN, ST)                                           \
+  hipLaunchKernelGGL((k_aead_tile<DECRYPT, LEN, false, kTileDesc>), grid, bt, 0, ST, a); \
   a.cls = kMCls0 + C;                                                          \
+  a.cls2 = -1;                                                                 \
   hipLaunchKernelGGL((k_aead_mtile<DECRYPT, LEN, kMTDesc>), grid, bt, 0, ST, a);
+#else
+#define NOISE_DESC_CAP(C, LEN, ST)                                             \
+  a.cls = C;                                                                   \
+  a.cls2 = kMCls0 + C;                                                         \
+  hipLaunchKernelGGL((k_aead_mtile<DECRYPT, LEN, kMTDesc>), grid, bt, 0, ST, a);
+#endif
   // the long records' tails (len % 1024 bytes) as masked 1 KiB tile units
   TileArgs at = a;
   at.tails = tails;
@@ -987,18 +1001,26 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   NOISE_DESC_BIG(ax.aux3)
   if ((e = hipEventRecord(ax.big, ax.aux3)) != hipSuccess) return e;
   if (!DECRYPT) {
-    // companion: dense tile classes first, the long-latency tails last (they
-    // then overlap the segment kernel's drain; tails first: -3..5 %)
+    // companion: the small classes and the generic kernel; the tails (masked
+    // 1 KiB units) on companion 2 from the prep event.  A/B (env
+    // NOISE_AB_ENC_TAILS=1): the tails last on the companion instead
+    static const bool tails_after = [] {
+      const char *v = std::getenv("NOISE_AB_ENC_TAILS");
+      return v && v[0] == '1';
+    }();
     NOISE_DESC_TILES()
-    if ((e = hipStreamWaitEvent(ax.aux, ax.prep, 0)) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_aead_mtile<false, 1024, kMTTail>), grid, bt, 0, ax.aux, at);
-    if ((e = hipEventRecord(ax.join, ax.aux)) != hipSuccess) return e;
+    hipStream_t ts = tails_after ? ax.aux : ax.aux2;
+    if ((e = hipStreamWaitEvent(ts, ax.prep, 0)) != hipSuccess) return e;
+    hipLaunchKernelGGL((k_aead_mtile<false, 1024, kMTTail>), grid, bt, 0, ts, at);
+    if ((e = hipEventRecord(ax.join, ts)) != hipSuccess) return e;
+    if (!tails_after && (e = hipEventRecord(ax.join2, ax.aux)) != hipSuccess) return e;
     // caller: every full segment of every long record, then the tags
     hipLaunchKernelGGL((k_aead_tile<DECRYPT, 1024, false, kTileSeg>), gseg, bt, 0, stream, a);
     if ((e = hipStreamWaitEvent(stream, ax.join, 0)) != hipSuccess) return e;
     hipLaunchKernelGGL((k_seg_finalize_w<DECRYPT, NOISE_FIN_W>), gfin, bt, 0, stream, fin, rt, ta.partial,
                        ta.partial_hi, hdr_w, in, out, status, -1);
     if ((e = hipStreamWaitEvent(stream, ax.big, 0)) != hipSuccess) return e;
+    if (!tails_after && (e = hipStreamWaitEvent(stream, ax.join2, 0)) != hipSuccess) return e;
     return hipGetLastError();
   }
   // decrypt.  Companion: the tails' Poly1305 first (the first tag check
@@ -1038,8 +1060,7 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
     atc.tail_split = chunks > 1 ? hdr->tsplit : nullptr;
     hipLaunchKernelGGL((k_aead_mtile<true, 1024, kMTTailXor>), grid, bt, 0, ax.aux, atc);
   }
-#undef NOISE_DESC_TILE
-#undef NOISE_DESC_MTILE
+#undef NOISE_DESC_CAP
 #undef NOISE_DESC_TILES
 #undef NOISE_DESC_BIG
   if ((e = hipEventRecord(ax.xdone, ax.aux2)) != hipSuccess) return e;

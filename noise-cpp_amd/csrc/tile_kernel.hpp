@@ -157,7 +157,8 @@ struct TileArgs {
   const unsigned long long *cls_base;  // kTileDesc: class start in idx (device)
   const unsigned long long *counts;    // kTileDesc: per-class counts (device)
   int cls;                       // kTileDesc: this launch's class
-  const SegEntry *segs;          // kTileSeg
+  int cls2;                      // kMTDesc: the ragged class stored right after cls in idx, or -1
+  const SegEntry *segs;         // kTileSeg
   const SegRec *rt;              // kTileSeg
   const unsigned long long *seg_split;  // kTileSeg*: chunk boundaries (device), or null
   int chunk;                     // kTileSeg*: this launch's chunk of seg_split

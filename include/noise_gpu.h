@@ -91,8 +91,12 @@ int noise_gpu_device_count(int *count);
  * out-of-place output (no unauthenticated plaintext is left behind).
  * 16-byte aligned pointers/strides, ad_len == 0 and len in {64, 128, 192,
  * 256, 512, 1024, 2048, 4096, 8192, 16384} run on the LDS-staged tile kernel
- * (the hot path); other shapes one record per lane (vector path when 16-byte
- * aligned with len % 16 == 0, byte-granular otherwise).
+ * (the hot path); any other len of 1..16384 with 16-byte aligned pointers
+ * and strides and no AD on the masked tile kernel, at the smallest tile
+ * capacity >= len (the powers of two above and 320, 384, 448, 768, 1280,
+ * 1536, 1792, 2304, 2560, 3072, 5120); other shapes (AD, unaligned records,
+ * len > 16384) one record per lane (vector path when 16-byte aligned with
+ * len % 16 == 0, byte-granular otherwise).
  * Key handling: h_key is copied into the kernel's argument block (kernarg
  * memory) by value, so the 32-byte key stays in that launch's kernarg
  * segment after the call, like any kernel argument; the runtime reuses,
@@ -122,19 +126,26 @@ int noise_gpu_decrypt_uniform(const uint8_t h_key[32], uint64_t nonce0,
  * (nothing written; decrypt status NOISE_GPU_REC_BAD_KEY).
  * Batches of >= 2048 records are load-balanced on the device, stream-ordered
  * (no host synchronisation): records are sorted by class and each class
- * runs its own kernel -- 16-byte aligned AD-free records of 64, 128, 192,
- * 256, 512, 1024, 2048, 4096, 8192 and 16384 bytes on the LDS-staged tile
- * kernel (a record up to 16 KiB whole in one wave); other aligned AD-free
- * records of 1024..65535 bytes (any length) cut into 1 KiB segments that ONE
- * tile-kernel launch processes, plus a tail kernel and a per-record finalize
- * (tag); everything else one lane per record.  Every path checks a record's
+ * runs its own kernel -- 16-byte aligned AD-free records of any length up to
+ * 16384 bytes on the LDS-staged masked tile kernel, one launch per tile
+ * capacity (64, 128, 192, 256, 512 B, 1, 2, 4, 8, 16 KiB: the smallest that
+ * holds the record; a record sits whole in one wave, and decrypt reads its
+ * ciphertext once); aligned AD-free records of 16385..65535 bytes cut into
+ * 1 KiB segments that ONE tile-kernel launch processes, plus their tails
+ * (len % 1024, masked 1 KiB tile units) and a per-record finalize (tag);
+ * everything else one lane per record.  Every path checks a record's
  * tag before any of its plaintext is stored (crypto_aead_read,
  * monocypher.c:2912-2929): the tile classes and the one-lane-per-record path
  * per record; a segmented (>= 1 KiB) record by a Poly1305 pass over its
  * ciphertext and the finalize's tag check, after which a keystream pass
  * writes the plaintext of the records that verified -- the output range of a
  * failed record never holds a byte of its plaintext, not even transiently.
- * Scratch is a grow-only device buffer per (device, stream). */
+ * Scratch is a grow-only device buffer per (device, stream).  The classes
+ * run on three companion streams the library creates per (device, stream)
+ * and joins back with events (no host synchronisation); with the caller's
+ * stream that is four HIP streams, the runtime's default number of hardware
+ * queues per process (GPU_MAX_HW_QUEUES = 4): further streams of the caller's
+ * own share those queues with them. */
 int noise_gpu_encrypt_records(const uint8_t *d_keys, uint32_t nkeys,
                               const noise_gpu_record *d_recs, uint64_t nrec,
                               const uint8_t *d_in, uint8_t *d_out,

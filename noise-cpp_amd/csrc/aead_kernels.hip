@@ -146,7 +146,14 @@ hipError_t launch_aead_uniform(bool decrypt, const uint32_t key[8],
   }
   // any other length up to 16 KiB with 16-byte aligned bases and strides:
   // the masked tile kernel at the smallest tile capacity >= len
-  // (mtile_kernel.hpp)
+  // (mtile_kernel.hpp).  Capacities between the
+  // powers of two: one lane of 5 .. 7 chunks per record (320 .. 448 B), or
+  // G = 3, 5, 6, 7, 9, 10, 12, 20 lanes of 4 chunks with 60-63 of 64 lanes
+  // working.  The cost of a record ~ capacity x 64 / working lanes rises with
+  // the capacity along this list, so the smallest that holds len is the
+  // cheapest.  (Not listed: 3840, 5376, 7680 -- they idle enough lanes to
+  // cost as much as the next power of two -- and nothing between 8 and 16 KiB,
+  // where a tile holds one record and the idle lanes would be 1/8 .. 1/2.)
   const bool al = ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out) | in_stride |
                     out_stride) & 15u) == 0;
   if (al && ad_len == 0 && len >= 1 && len <= 16384) {
@@ -164,7 +171,7 @@ hipError_t launch_aead_uniform(bool decrypt, const uint32_t key[8],
     ta.chunk = -1;
 #define NOISE_MTILE(LEN)                                                       \
     if (len <= LEN) {                                                          \
-      constexpr uint64_t rps = LEN > 2048 ? 64 * 2048 / LEN : 64;              \
+      constexpr uint64_t rps = MTileCfg<LEN>::RPS;                             \
       const dim3 gm((unsigned)((nrec + rps - 1) / rps)), bm(64);               \
       if (decrypt) hipLaunchKernelGGL((k_aead_mtile<true, LEN, kMTUniform>), gm, bm, 0, stream, ta); \
       else hipLaunchKernelGGL((k_aead_mtile<false, LEN, kMTUniform>), gm, bm, 0, stream, ta);        \
@@ -174,10 +181,21 @@ hipError_t launch_aead_uniform(bool decrypt, const uint32_t key[8],
     NOISE_MTILE(128)
     NOISE_MTILE(192)
     NOISE_MTILE(256)
+    NOISE_MTILE(320)
+    NOISE_MTILE(384)
+    NOISE_MTILE(448)
     NOISE_MTILE(512)
+    NOISE_MTILE(768)
     NOISE_MTILE(1024)
+    NOISE_MTILE(1280)
+    NOISE_MTILE(1536)
+    NOISE_MTILE(1792)
     NOISE_MTILE(2048)
+    NOISE_MTILE(2304)
+    NOISE_MTILE(2560)
+    NOISE_MTILE(3072)
     NOISE_MTILE(4096)
+    NOISE_MTILE(5120)
     NOISE_MTILE(8192)
     NOISE_MTILE(16384)
 #undef NOISE_MTILE

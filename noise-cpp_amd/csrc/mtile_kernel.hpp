@@ -136,11 +136,67 @@ __device__ __forceinline__ void store_head(uint8_t *p, uint4 v, uint32_t n) {
 #endif
 }
 
+// Tile shape of capacity L (a multiple of 64).  Up to 7 chunks (448 B): one
+// lane per record, CPL = L / 64.  Above: lanes of 4 chunks (256 B), G = L / 256
+// lanes per record -- G need not divide 64 (1280 B: G = 5, 12 records on 60
+// lanes; lanes past RPT G idle), which gives capacities between the powers of
+// two (the uniform dispatch, aead_kernels.hip).
+template <int L>
+struct MTileCfg {
+  static constexpr int NCH = L / 64;
+  static constexpr int G = NCH <= 7 ? 1 : NCH / 4;
+  static constexpr int CPL = NCH / G;
+  static constexpr int BPL = 4 * CPL;
+  static constexpr int RPT = 64 / G;
+  static constexpr int LANES = RPT * G;  // working lanes
+  static constexpr int SPR = L / 16;
+  static constexpr int S = 4 * CPL;      // slots of one lane's span
+  static constexpr int REC_SLOTS = RPT * SPR;
+  static constexpr int NSLOT = REC_SLOTS + RPT;
+  static constexpr int LOG2G = G <= 1 ? 0 : G <= 2 ? 1 : G <= 4 ? 2 : G <= 8 ? 3 : G <= 16 ? 4 : G <= 32 ? 5 : 6;
+  // records per super-tile (one key lane each): 64, at most 128 KiB for
+  // capacities above 2 KiB (batches of large records make waves), a
+  // multiple of RPT
+  static constexpr int RPS0 = L > 2048 ? 64 * 2048 / L : 64;
+  static constexpr int RPS = RPS0 >= RPT ? RPS0 / RPT * RPT : RPT;
+  static_assert(L % 64 == 0 && L >= 64 && L <= 16384 && (NCH <= 7 || NCH % 4 == 0), "capacity");
+};
+
+// slot of piece g (lane spans of S slots; pieces of a span stay in it).
+// Spans of 4, 8, 16 slots: swz<256> (conflict-free ds_read_b128).  12, 20,
+// 24, 28 (one lane of 3, 5, 6, 7 chunks): swz<256> is 3-4-way conflicted
+// there, so the span is rotated by k(l) = (l >> 2) & 3 ((l >> 1) & 7 for 24):
+// the 16 lanes of a read group then hit 16 distinct bank quads.
+template <int S>
+__device__ __forceinline__ uint32_t rot_k(uint32_t l) {
+  return S == 24 ? (l >> 1) & 7u : (l >> 2) & 3u;
+}
+template <int S>
+__device__ __forceinline__ uint32_t mslot(uint32_t g) {
+  if constexpr (S == 4 || S == 8 || S == 16) {
+    return swz<256>(g);
+  } else {
+    const uint32_t l = g / S, i = g % S, t = i + rot_k<S>(l);
+    return (uint32_t)S * l + (t >= (uint32_t)S ? t - S : t);
+  }
+}
+// piece held by slot s (mslot's inverse)
+template <int S>
+__device__ __forceinline__ uint32_t mpiece(uint32_t s) {
+  if constexpr (S == 4 || S == 8 || S == 16) {
+    return swz<256>(s);
+  } else {
+    const uint32_t l = s / S, i = s % S, t = i + (uint32_t)S - rot_k<S>(l);
+    return (uint32_t)S * l + (t >= (uint32_t)S ? t - S : t);
+  }
+}
+
 template <bool DECRYPT, int L, int MODE>
 __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) {
-  using C = TileCfg<L, 256>;
-  constexpr int G = C::G, CPL = C::CPL, BPL = C::BPL, SPR = C::SPR, RPT = C::RPT;
+  using C = MTileCfg<L>;
+  constexpr int G = C::G, CPL = C::CPL, BPL = C::BPL, SPR = C::SPR, RPT = C::RPT, S = C::S;
   constexpr int REC_SLOTS = C::REC_SLOTS, NSLOT = C::NSLOT;
+  constexpr bool IDLE = C::LANES < 64;  // lanes past RPT G do no work
   constexpr int ZSLOT = NSLOT, JSLOT = NSLOT + 1;  // zero slot, junk slot (absent XOR writes)
   constexpr bool TAIL = MODE >= kMTTail;
   constexpr bool KEYED = MODE != kMTUniform;
@@ -155,21 +211,26 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
   constexpr int OPR = TAG_OUT ? SPR + 1 : SPR;  // output pieces of a full record
   constexpr int KPR = SPR / 64;                 // KiB per record (L >= 1024)
   constexpr bool WHOLE_KIB = SPR % 64 == 0;
+  static_assert(!WHOLE_KIB || S == 16, "whole-KiB records: lane spans of 16 slots");
   // 256 / 512-byte classes: a DMA or store instruction covers RPI = 64 / SPR
   // (4, 2) whole records -- their lengths and offsets come from RPI
   // v_readlanes and a per-lane select instead of a shuffle per piece (the
   // uniform mode computes them per lane: no shuffles to save)
   constexpr bool SUB_KIB = KEYED && (SPR == 16 || SPR == 32);
+  static_assert(!SUB_KIB || S == 16, "256 / 512-byte records: lane spans of 16 slots");
   constexpr int RPI = SUB_KIB ? 64 / SPR : 1;
   // records per super-tile: 64 (one key lane each), at most 128 KiB for
   // classes of 4 KiB and up (so that batches of large records make waves)
-  constexpr int RPS = L > 2048 ? 64 * 2048 / L : 64;
+  constexpr int RPS = C::RPS;
   constexpr int NTS = RPS / RPT;
   static_assert(NTS >= 1 && RPS % RPT == 0, "super-tile shape");
   __shared__ uint4 lds[NSLOT + 2];
   uint4 *lb = lds;
   const uint32_t lane = threadIdx.x;
-  const uint32_t rho = lane / G, j = lane % G;
+  // idle lanes (past RPT G) shadow record 0: they read its tile, write the
+  // junk slot, and are never valid
+  const uint32_t rho = lane < (uint32_t)C::LANES ? lane / G : 0u, j = lane % G;
+  const bool idle = IDLE && lane >= (uint32_t)C::LANES;
   if (lane == 0) lds[ZSLOT] = make_uint4(0u, 0u, 0u, 0u);  // never overwritten
   // mtab[n]: the mask keeping the first n (0..16) bytes of a 16-byte piece
   __shared__ uint4 mtab[17];
@@ -418,7 +479,7 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
           const uint32_t s = 64u * q + lane;
           uint32_t r, p;
           if (s < (uint32_t)REC_SLOTS) {
-            const uint32_t g = swz<256>(s);
+            const uint32_t g = mpiece<S>(s);
             r = g / SPR;
             p = g % SPR;
           } else {  // tag slots
@@ -444,7 +505,7 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
       kr[3] = otk[3] & 0x0ffffffcu;
       kss[0] = otk[4]; kss[1] = otk[5]; kss[2] = otk[6]; kss[3] = otk[7];
       if (G > 1) {
-        static_assert(G == 1 || C::LOG2BPL == 4, "lanes of 16 Poly1305 blocks");
+        static_assert(G == 1 || BPL == 16, "lanes of 16 Poly1305 blocks");
         F26 x = to26(kr[0], kr[1], kr[2], kr[3], 0u);
         const F26 x1 = x;
         const F26 x2 = mul26(x1, x1), x4 = mul26(x2, x2), x8 = mul26(x4, x4);
@@ -473,7 +534,7 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
       wait_vmem();
       wave_lds_fence();
       const uint32_t src = (uint32_t)t * RPT + rho;  // key lane of my record
-      const bool valid = rho < nv;
+      const bool valid = !idle && rho < nv;
       // ---- this lane's record ------------------------------------------
       const uint32_t rlen = len_v(src);
       const uint32_t P = (rlen + 15u) >> 4, Cc = (rlen + 63u) >> 6;
@@ -481,7 +542,7 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
       const int dc = (int)(L / 64) - (int)Cc;  // leading absent chunks
       const uint32_t rbase = rho * SPR;
       auto pslot = [&](uint32_t i) -> uint32_t {  // record piece i (0 .. SPR) -> slot
-        return i < (uint32_t)SPR ? swz<256>(rbase + i) : (uint32_t)REC_SLOTS + rho;
+        return i < (uint32_t)SPR ? mslot<S>(rbase + i) : (uint32_t)REC_SLOTS + rho;
       };
       Poly1305 p;
       p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0u;
@@ -547,7 +608,7 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
         const bool last = kk == CPL - 1;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const uint32_t slot = (EX || c >= 0) ? swz<256>(rbase + 4u * (uint32_t)c + (uint32_t)q) : (uint32_t)JSLOT;
+          const uint32_t slot = (EX || c >= 0) && !idle ? mslot<S>(rbase + 4u * (uint32_t)c + (uint32_t)q) : (uint32_t)JSLOT;
           const uint4 v = lb[slot];
           uint4 o = v;
           if (DO_XOR) {
@@ -615,11 +676,24 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
           }
           h = mul26(h, f);
         }
+        if constexpr ((G & (G - 1)) == 0) {  // butterfly: every lane of the record gets the sum
 #pragma unroll
-        for (int b = 0; b < C::LOG2G; ++b) {
-          if (b == 4) carry26(h);
+          for (int b = 0; b < C::LOG2G; ++b) {
+            if (b == 4) carry26(h);
 #pragma unroll
-          for (int i = 0; i < 5; ++i) h.a[i] += __shfl_xor(h.a[i], 1 << b);
+            for (int i = 0; i < 5; ++i) h.a[i] += __shfl_xor(h.a[i], 1 << b);
+          }
+        } else {  // G lanes not a power of two: a tree into lane j = 0 (the only user)
+#pragma unroll
+          for (int b = 0; b < C::LOG2G; ++b) {
+            if (b == 4) carry26(h);
+            const bool in = j + (1u << b) < (uint32_t)G;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+              const uint32_t w = (uint32_t)__shfl((int)h.a[i], (int)((lane + (1u << b)) & 63u));
+              h.a[i] += in ? w : 0u;
+            }
+          }
         }
         carry26(h);
         carry26(h);
@@ -717,7 +791,7 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
           pc = g % OPR;
           ok = (RPT * OPR) % 64 == 0 || g < (uint32_t)(RPT * OPR);
           if (!ok) r = 0;
-          slot = pc < (uint32_t)SPR ? swz<256>(r * SPR + pc) : (uint32_t)REC_SLOTS + r;
+          slot = pc < (uint32_t)SPR ? mslot<S>(r * SPR + pc) : (uint32_t)REC_SLOTS + r;
         }
       };
       const uint32_t pr = lane < (uint32_t)RPT ? lane : 0u;  // the partial piece's record
@@ -740,7 +814,7 @@ __global__ __launch_bounds__(64) NOISE_OCC2 void k_aead_mtile(const TileArgs a) 
           if (!EX) {
             const uint32_t ob = len_v((uint32_t)t * RPT + pr) + (TAG_OUT ? 16u : 0u);
             const uint32_t pp = ob >> 4;  // its piece index
-            const uint32_t slot = pp < (uint32_t)SPR ? swz<256>(pr * SPR + pp) : (uint32_t)REC_SLOTS + pr;
+            const uint32_t slot = pp < (uint32_t)SPR ? mslot<S>(pr * SPR + pp) : (uint32_t)REC_SLOTS + pr;
             pv = lb[(ob & 15u) ? slot : (uint32_t)ZSLOT];
           }
           wait_lds();  // every LDS read of this tile done

@@ -29,7 +29,6 @@
 // Small batches (< kClassifyMin records) skip all this and run the generic
 // kernel directly (latency of single records from CipherState).
 // Scratch is a grow-only device buffer cached per (device, stream).
-#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -1001,26 +1000,21 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   NOISE_DESC_BIG(ax.aux3)
   if ((e = hipEventRecord(ax.big, ax.aux3)) != hipSuccess) return e;
   if (!DECRYPT) {
-    // companion: the small classes and the generic kernel; the tails (masked
-    // 1 KiB units) on companion 2 from the prep event.  A/B (env
-    // NOISE_AB_ENC_TAILS=1): the tails last on the companion instead
-    static const bool tails_after = [] {
-      const char *v = std::getenv("NOISE_AB_ENC_TAILS");
-      return v && v[0] == '1';
-    }();
+    // companion: dense tile classes first, the tails (masked 1 KiB units)
+    // last.  Round 6 A/B, the tails on companion 2 from the prep event
+    // instead: config 4 1391-1395 against 1408-1409 GiB/s (exact lengths),
+    // 1330-1336 against 1339-1351 (jittered), same box, alternating
+    // (profiles/round6/ab/enc_tails.md)
     NOISE_DESC_TILES()
-    hipStream_t ts = tails_after ? ax.aux : ax.aux2;
-    if ((e = hipStreamWaitEvent(ts, ax.prep, 0)) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_aead_mtile<false, 1024, kMTTail>), grid, bt, 0, ts, at);
-    if ((e = hipEventRecord(ax.join, ts)) != hipSuccess) return e;
-    if (!tails_after && (e = hipEventRecord(ax.join2, ax.aux)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(ax.aux, ax.prep, 0)) != hipSuccess) return e;
+    hipLaunchKernelGGL((k_aead_mtile<false, 1024, kMTTail>), grid, bt, 0, ax.aux, at);
+    if ((e = hipEventRecord(ax.join, ax.aux)) != hipSuccess) return e;
     // caller: every full segment of every long record, then the tags
     hipLaunchKernelGGL((k_aead_tile<DECRYPT, 1024, false, kTileSeg>), gseg, bt, 0, stream, a);
     if ((e = hipStreamWaitEvent(stream, ax.join, 0)) != hipSuccess) return e;
     hipLaunchKernelGGL((k_seg_finalize_w<DECRYPT, NOISE_FIN_W>), gfin, bt, 0, stream, fin, rt, ta.partial,
                        ta.partial_hi, hdr_w, in, out, status, -1);
     if ((e = hipStreamWaitEvent(stream, ax.big, 0)) != hipSuccess) return e;
-    if (!tails_after && (e = hipStreamWaitEvent(stream, ax.join2, 0)) != hipSuccess) return e;
     return hipGetLastError();
   }
   // decrypt.  Companion: the tails' Poly1305 first (the first tag check

@@ -3,7 +3,9 @@ record lengths OFF the exact tile table, which before round 6 fell to one
 lane per record.
 
 Uniform batches (noise_gpu_encrypt_uniform / _decrypt_uniform) with 16-byte
-aligned bases and strides and lengths 1 .. 16383 around every class edge: a
+aligned bases and strides and lengths 1 .. 16383 around every class edge
+(the power-of-two tiles and the capacities between them: 320 .. 448 B with
+one lane per record, 768 .. 5120 B with 3 .. 20 lanes and idle ones): a
 lone record, a partial tile and several tiles / super-tiles; three layouts
 (tight = strides rounded up to 16, padded = with gaps, in place).  Every
 record is compared with the CPU oracle (oracle_check_uniform), the bytes
@@ -25,6 +27,9 @@ torch = pytest.importorskip("torch")
 
 LENGTHS = [1, 15, 17, 63, 65, 100, 129, 191, 193, 255, 257, 300, 511, 513, 700, 1000, 1023, 1025,
            1040, 1400, 2047, 2049, 3000, 4095, 4097, 5000, 8191, 8193, 9000, 16000, 16383]
+# the capacities between the powers of two (aead_kernels.hip): each full, and
+# one byte past it (the next class)
+LENGTHS += [320, 321, 384, 448, 449, 768, 769, 1280, 1536, 1792, 1793, 2304, 2560, 3072, 3073, 5120, 5121]
 NRECS = [1, 65, 200]
 LAYOUTS = ["tight", "padded", "in_place"]
 FILL = 0xEE

@@ -164,11 +164,12 @@ int main(int argc, char **argv) {
   std::vector<uint32_t> lens;
   for (int i = 2; i < argc; ++i) lens.push_back((uint32_t)std::strtoul(argv[i], nullptr, 0));
   if (lens.empty())
-    lens = {1, 15, 16, 17, 33, 63, 65, 100, 127, 129, 191, 193, 255, 257, 300, 400, 511, 513, 700, 1000, 1023,
-            1025, 1040, 1400, 2047, 2049, 3000, 4095, 5000, 8191, 9000, 16000, 16383};
+    lens = {1, 15, 16, 17, 33, 63, 65, 100, 127, 129, 191, 193, 255, 257, 300, 321, 384, 400, 449, 511, 513,
+            700, 769, 1000, 1023, 1025, 1040, 1281, 1400, 1537, 1793, 2047, 2049, 2305, 2561, 3000, 3073, 4095,
+            4097, 5000, 5121, 8191, 9000, 16000, 16383};
   for (uint32_t L : lens) {
     // a few tiles and a partial one (records per tile: 64 / max(1, L / 256))
-    const uint64_t rpt = L >= 256 ? 64 / ((L + 255) / 256 > 64 ? 64 : (L + 255) / 256) : 64;
+    const uint64_t rpt = L >= 256 ? 64 / ((L + 255) / 256 > 64 ? 64 : (L + 255) / 256) : 64;  // ~ (capacity classes)
     const uint64_t R = L > 4096 ? 6 : rpt * 2 + 3;
     const long o0 = g_outside.load(), u0 = g_unverified.load();
     run(L, seed + L, false, R);

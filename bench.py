@@ -631,10 +631,10 @@ def make_workload(cfg, args, rank, world, stream):
                 "metric": metric, "config": cfgd, "pt_bytes": pt_bytes,
                 "enc_bytes": pt_bytes + ct_bytes + 48 * R, "dec_bytes": pt_bytes + ct_bytes + 49 * R,
                 "read_bytes": (pt_bytes + 48 * R, ct_bytes + 48 * R),
-                "knames": (("noise_amd::k_cls_", "noise_amd::k_seg_prep", "noise_amd::k_seg_tail<false",
+                "knames": (("noise_amd::k_cls_", "noise_amd::k_seg_prep", "noise_amd::k_aead_mtile<false",
                             "noise_amd::k_seg_finalize_w<false", "noise_amd::k_aead_tile<false",
                             "noise_amd::k_aead_records<false"),
-                           ("noise_amd::k_cls_", "noise_amd::k_seg_prep", "noise_amd::k_seg_tail<true",
+                           ("noise_amd::k_cls_", "noise_amd::k_seg_prep", "noise_amd::k_aead_mtile<true",
                             "noise_amd::k_seg_finalize_w<true", "noise_amd::k_aead_tile<true",
                             "noise_amd::k_aead_records<true")),
                 "call_level": True, "oracle": oracle,

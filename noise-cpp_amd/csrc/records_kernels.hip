@@ -161,7 +161,11 @@ __device__ __forceinline__ int record_class(const noise_gpu_record &d, const uin
   // every other length up to 16 KiB: the masked tile class of the smallest
   // capacity that holds it -- the record still sits whole in one wave's
   // tile, so decrypt checks its tag there and reads the ciphertext once
-  if (d.len <= 16384u) {
+  // (8 KiB, 12 KiB]: the 16 KiB tile would run at <= 75 % of its capacity
+  // (one record per tile); the segment path is faster there (9000 B: 808
+  // against 693 GiB/s: before/sweep.jsonl, final/sweep_records_grid.jsonl
+  // under profiles/round6)
+  if (d.len <= 16384u && !(d.len > 8192u && d.len <= 12288u)) {
     const uint32_t n = d.len;
     const int c = n <= 64u ? 0 : n <= 128u ? 1 : n <= 192u ? 2 : n <= 256u ? 3 : n <= 512u ? 4
                 : n <= 1024u ? 5 : n <= 2048u ? 6 : n <= 4096u ? 7 : n <= 8192u ? 8 : 9;
@@ -932,6 +936,10 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   if (e != hipSuccess) return e;
   const dim3 bt(64);
   const dim3 grid(capped((nrec + 63) / 64, NOISE_GRID_CAP));
+  // a class launch: enough workgroups for the whole batch in the class (its
+  // size is on the device), RPS records per super-tile -- 8 for 16 KiB, so a
+  // batch of 100 K such records makes 12.5 K waves, not 1.6 K
+  auto desc_grid = [nrec](uint64_t rps) { return dim3(capped((nrec + rps - 1) / rps, NOISE_GRID_CAP)); };
   SegRec *rt = const_cast<SegRec *>(ta.rt);
   // fork right after the classifier: the small classes and the generic
   // kernel need nothing else; the tails also need k_seg_prep (prep event)
@@ -953,10 +961,7 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   // launches per capacity (the exact tile kernel, then the masked one) left
   // nearly empty launches queued between full ones: a capped grid of single
   // -wave workgroups waits for CU slots even when it has no work (config-4
-  // traces, profiles/round6/ab).  NOISE_DESC_SPLIT=1 keeps the split form.
-#ifndef NOISE_DESC_SPLIT
-#define NOISE_DESC_SPLIT 0
-#endif
+  // traces, profiles/round6/merged/cfg4_*_timeline.txt).
 #define NOISE_DESC_BIG(ST)                                                     \
   NOISE_DESC_CAP(9, 16384, ST)                                                 \
   NOISE_DESC_CAP(8, 8192, ST)                                                  \
@@ -971,19 +976,10 @@ static hipError_t launch_classes(const TileArgs &ta, uint64_t nrec, const RecHdr
   NOISE_DESC_CAP(5, 1024, ax.aux)                                              \
   hipLaunchKernelGGL((k_aead_records<DECRYPT>), gg, dim3(kGenBlock), 0, ax.aux, keys, nkeys, recs,  \
                      nrec, idx, hdr, in, out, ad, status);
-#if NOISE_DESC_SPLIT
-#define NOISE_DESC_CAP(C, LEN, ST)                                             \
-  a.cls = C;                                                                   \
-  hipLaunchKernelGGL((k_aead_tile<DECRYPT, LEN, false, kTileDesc>), grid, bt, 0, ST, a); \
-  a.cls = kMCls0 + C;                                                          \
-  a.cls2 = -1;                                                                 \
-  hipLaunchKernelGGL((k_aead_mtile<DECRYPT, LEN, kMTDesc>), grid, bt, 0, ST, a);
-#else
 #define NOISE_DESC_CAP(C, LEN, ST)                                             \
   a.cls = C;                                                                   \
   a.cls2 = kMCls0 + C;                                                         \
-  hipLaunchKernelGGL((k_aead_mtile<DECRYPT, LEN, kMTDesc>), grid, bt, 0, ST, a);
-#endif
+  hipLaunchKernelGGL((k_aead_mtile<DECRYPT, LEN, kMTDesc>), desc_grid(MTileCfg<LEN>::RPS), bt, 0, ST, a);
   // the long records' tails (len % 1024 bytes) as masked 1 KiB tile units
   TileArgs at = a;
   at.tails = tails;

@@ -422,7 +422,8 @@ def test_whole_record_classes_tamper(oracle, in_place):
 
 
 RAGGED = [1, 33, 64, 65, 100, 127, 129, 191, 193, 255, 257, 300, 480, 511, 513, 700, 961, 1000, 1023, 1025,
-          1040, 1400, 1985, 2047, 2049, 3000, 4033, 4095, 4097, 5000, 8129, 8191, 8193, 9000, 16000, 16321,
+          1040, 1400, 1985, 2047, 2049, 3000, 4033, 4095, 4097, 5000, 8129, 8191, 8193, 9000, 12288, 12289,
+          16000, 16321,
           16383, 16385, 17000, 32705, 32767, 65456, 65500, 65519]
 
 

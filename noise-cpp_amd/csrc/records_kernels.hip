@@ -9,22 +9,25 @@
 //      one scan -- no contended atomics;
 //   2. one launch per class, each reading its slice and count from device
 //      memory:
-//        - tile classes: 16-byte aligned, AD-free records of 64, 128, 192,
-//          256, 512, 1024 bytes -> the LDS-staged tile kernel (tile_kernel.hpp,
-//          kTileDesc);
-//        - long records: 16-byte aligned, AD-free, 1024 <= len <= 65535
-//          (any length) -> cut into 1 KiB segments + a tail.  k_seg_prep
+//        - tile classes: 16-byte aligned, AD-free records of any length up
+//          to 16 KiB, by the smallest capacity (64 .. 16384 B) that holds
+//          them -> the LDS-staged masked tile kernel (mtile_kernel.hpp,
+//          kMTDesc), one launch per capacity for its exact-size and ragged
+//          records;
+//        - long records: 16-byte aligned, AD-free, 16 KiB < len <= 65535
+//          (and 8 KiB < len <= 12 KiB, see record_class) -> cut into 1 KiB
+//          segments + a tail (masked 1 KiB tile units).  k_seg_prep
 //          derives each record's one-time key and r powers, ONE tile-kernel
 //          launch (kTileSeg) encrypts every full segment of every long
 //          record -- uniform 1 KiB work units, whatever the size mix -- and
 //          k_seg_finalize_w combines the segments' Poly1305 partial sums with
 //          the tail's, the length block and the tag.  Decrypt verifies first:
-//          a Poly1305-only pass over the ciphertext (kTileSegPoly, kTailPoly),
+//          a Poly1305-only pass over the ciphertext (kTileSegPoly, kMTTailPoly),
 //          the finalize checks every tag, and only then the keystream pass
-//          (kTileSegXor, kTailXor) writes the plaintext of the records that
+//          (kTileSegXor, kMTTailXor) writes the plaintext of the records that
 //          verified -- no byte of a failed record's plaintext is ever stored;
-//        - generic: everything else (AD, odd lengths < 1 KiB, unaligned, bad
-//          key index, and long records beyond the segment scratch capacity)
+//        - generic: everything else (AD, unaligned, bad key index, > 65535
+//          bytes, and long records beyond the segment scratch capacity)
 //          -> one lane per record (chachapoly_device.hpp).
 // Small batches (< kClassifyMin records) skip all this and run the generic
 // kernel directly (latency of single records from CipherState).
@@ -900,13 +903,14 @@ static hipError_t aux_release(int dev, hipStream_t stream) {
 
 // After the classifier, two branches.  Encrypt:
 //   caller stream : k_seg_prep -+-> segment tile kernel (kTileSeg) --- join -> finalize
-//   companion     : (fork)  the five small tile classes, the generic kernel,
-//                   (wait prep) the tails (kTailFused) ------------^
-// The segment kernel is the long pole (~80 % of a config-4 call); the
-// companion branch's launches are short or under-filled (the tails kernel has
-// one lane per tail) and overlap it instead of following it.  The tails go
-// last so their long per-lane chains fill the segment kernel's drain
-// (profiles/round2/ab/ab_experiments.md).
+//   companion     : (fork)  the six small tile classes, the generic kernel,
+//                   (wait prep) the tails (kMTTail) ---------------^
+//   companion 3   : (fork)  the 2 .. 16 KiB tile classes ---------------> end
+// The segment kernel is the long pole; the companion branches overlap it
+// instead of following it.  The tails go last on the companion, so they
+// fill the segment kernel's drain (round 2, profiles/round2/ab/; round 6:
+// the tails on the idle companion 2 from the prep event were 1.5 % slower,
+// profiles/round6/ab/enc_tails.md).
 //
 // Decrypt checks every long record's tag BEFORE any of its plaintext is
 // written (crypto_aead_read, monocypher.c:2912-2929): a Poly1305 pass reads

@@ -91,7 +91,7 @@ __device__ __forceinline__ void wave_lds_fence() {
 enum TileMode : int {
   kTileUniform = 0,   // one key, nonce0 + i, record i at in + i*in_stride
   kTileSessions = 1,  // key row keys[key_idx[i]], nonce nonces[i], strided
-  kTileDesc = 2,      // descriptor recs[idx[base + i]] (records API class)
+  // 2: round 5's descriptor classes, now k_aead_mtile's kMTDesc
   kTileSeg = 3,       // 1 KiB segment g of a long record (segs[g] -> SegRec):
                       // ciphertext + Poly1305 partial sum, no tag (encrypt)
   kTileSegPoly = 4,   // decrypt pass 1: the segment's Poly1305 partial sum of
@@ -110,9 +110,9 @@ enum TileMode : int {
 // load-balanced launch -- and leaves the segment's Poly1305 Horner sum
 //   P_s = sum_{i<64} m_{64s+i} r^(64-i)
 // in SegPartial.  The finalize kernel combines h = sum_s P_s r^(64(nfull-1-s))
-// (Horner in R = r^64), appends the tail (k_seg_tail: the len % 1024 bytes
-// past the last full segment, one lane per tail) as h r^(tail blocks) +
-// P_tail, then the length block and the tag.
+// (Horner in R = r^64), appends the tail (the len % 1024 bytes past the last
+// full segment, masked 1 KiB tile units of k_aead_mtile) as h r^(tail blocks)
+// + P_tail, then the length block and the tag.
 struct SegRec {                  // one per long record, 256 B (two 128-B lines)
   uint64_t in_off, out_off, nonce, seg0;  // seg0: index of segment 0
   uint32_t k[8];                 // the record's key (copied from the key table)
@@ -145,18 +145,18 @@ struct TileArgs {
   uint64_t in_stride;  // kTileUniform / kTileSessions
   uint8_t *out;
   uint64_t out_stride;
-  uint8_t *status;    // decrypt: per record (kTileDesc: per descriptor)
+  uint8_t *status;    // decrypt: per record (kMTDesc: per descriptor)
   uint64_t nrec;      // kTileUniform / kTileSessions
   int in_place;       // kTileUniform / kTileSessions
-  uint32_t nkeys;     // kTileSessions / kTileDesc
+  uint32_t nkeys;     // kTileSessions / kMTDesc
   const uint8_t *keys;
   const uint32_t *key_idx;  // kTileSessions
   const uint64_t *nonces;   // kTileSessions
-  const noise_gpu_record *recs;  // kTileDesc
-  const uint32_t *idx;           // kTileDesc: class-sorted descriptor indices
-  const unsigned long long *cls_base;  // kTileDesc: class start in idx (device)
-  const unsigned long long *counts;    // kTileDesc: per-class counts (device)
-  int cls;                       // kTileDesc: this launch's class
+  const noise_gpu_record *recs;  // kMTDesc (mtile_kernel.hpp)
+  const uint32_t *idx;           // kMTDesc: class-sorted descriptor indices
+  const unsigned long long *cls_base;  // kMTDesc: class start in idx (device)
+  const unsigned long long *counts;    // kMTDesc: per-class counts (device)
+  int cls;                       // kMTDesc: this launch's class
   int cls2;                      // kMTDesc: the ragged class stored right after cls in idx, or -1
   const SegEntry *segs;         // kTileSeg
   const SegRec *rt;              // kTileSeg
@@ -173,23 +173,15 @@ struct TileArgs {
   const unsigned long long *nlong;      // kMTTail*: long records in the scratch (device)
 };
 
-// kTileDesc: the class's slice of the sorted index array; kTileSeg: all
-// segments
-template <int MODE>
-__device__ __forceinline__ void desc_class_range(const TileArgs &a,
-                                                 uint64_t &base, uint64_t &n) {
+// kTileSeg*: all segments, or chunk a.chunk of them
+__device__ __forceinline__ void seg_range(const TileArgs &a, uint64_t &base, uint64_t &n) {
   base = 0;
-  if (MODE >= kTileSeg) {
-    n = *a.nseg;
-    if (a.seg_split) {  // chunk c: [split[c], split[c + 1]), clamped to the segments there are
-      const uint64_t lo = a.seg_split[a.chunk], hi = a.seg_split[a.chunk + 1];
-      base = lo < n ? lo : n;
-      n = (hi < n ? hi : n) - base;
-    }
-    return;
+  n = *a.nseg;
+  if (a.seg_split) {  // chunk c: [split[c], split[c + 1]), clamped to the segments there are
+    const uint64_t lo = a.seg_split[a.chunk], hi = a.seg_split[a.chunk + 1];
+    base = lo < n ? lo : n;
+    n = (hi < n ? hi : n) - base;
   }
-  base = a.cls_base[a.cls];
-  n = a.counts[a.cls];
 }
 
 template <int L, bool DECRYPT, bool CONTIG, int MODE, int ABL, int SPAN>
@@ -236,8 +228,8 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
           lds_dma16_s(base, 16u * (r * (C::SPR + 1) + C::SPR), (lds_void *)(lds3 + 64 * q));
       }
     }
-  } else if (MODE >= kTileSeg || (MODE == kTileDesc && C::SPR % 64 == 0)) {
-    // whole KiB (segments, kTileDesc records of 1 KiB .. 16 KiB): DMA
+  } else if (MODE >= kTileSeg) {
+    // whole KiB (segments): DMA
     // instruction q moves KiB q % (SPR / 64) of unit q / (SPR / 64), so its
     // offset is wave-uniform -- read from the unit's key lane (v_readlane into
     // SGPRs) instead of a per-lane shuffle
@@ -273,7 +265,7 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
         p = C::SPR;
       }
       const uint8_t *rec_base;
-      if (MODE == kTileDesc || MODE >= kTileSeg) {  // offset of record r: key lane t*RPT + r
+      if (MODE >= kTileSeg) {  // offset of record r: key lane t*RPT + r
         const uint32_t src = t_rpt + (r < (uint32_t)C::RPT ? r : 0u);
         const uint64_t off = ((uint64_t)(uint32_t)__shfl((int)own_in_hi, src) << 32) |
                              (uint32_t)__shfl((int)own_in_lo, src);
@@ -287,12 +279,9 @@ __device__ __forceinline__ void tile_load(lds_u4 *lds3, const uint8_t *in,
   }
 }
 
-// MODE kTileSessions / kTileDesc: record i uses key row keys[key_idx] and
-// its own nonce; a key index outside the table makes the record fail
-// (nothing written; decrypt status NOISE_GPU_REC_BAD_KEY).  kTileDesc also
-// takes per-record offsets from the descriptor (16-byte aligned; the
-// classifier guarantees it) and is launched with a capped grid that strides
-// over the class's super-tiles.
+// MODE kTileSessions: record i uses key row keys[key_idx] and its own
+// nonce; a key index outside the table makes the record fail (nothing
+// written; decrypt status NOISE_GPU_REC_BAD_KEY).
 // kTileSeg (L = 1024): unit i is full segment i of a long record (SegEntry ->
 // SegRec): no key block (r and its powers come from the SegRec), ChaCha
 // counters 1 + 16 s + ..., no tag: the segment's Poly1305 partial sum goes to
@@ -365,12 +354,12 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
   // Strided layouts (in-place batches, padded strides) take it too: their
   // wire-order gather (a division by SPR + 1 and a 64-bit address per lane
   // and instruction) pushed the keyed encrypt kernels past 256 VGPRs, i.e.
-  // to one wave per SIMD.  Not kTileDesc / kTileSeg (RECQ below).
-  constexpr bool RECW = !DECRYPT && !SEG && MODE != kTileDesc && C::SPR >= 64 &&
+  // to one wave per SIMD.  Not kTileSeg (RECQ below).
+  constexpr bool RECW = !DECRYPT && !SEG && C::SPR >= 64 &&
                         C::SPR % 64 == 0;
   constexpr int NDATA = C::RPT * C::SPR / 64;
   constexpr int NOUT = RECW ? NDATA + 1 : (OUT_SLOTS + 63) / 64;  // store instructions
-  static_assert(!(CONTIG && (MODE == kTileDesc || SEG)), "descriptor tiles are strided");
+  static_assert(!(CONTIG && SEG), "segment tiles are strided");
   static_assert(!SEG || (L == 1024 && (SPAN == 256 || SPAN == 128)),
                 "segments are 1 KiB, 256 or 128 B per lane");
   static_assert(!SEG || !DO_POLY || SPAN == 256, "the SegRec holds the 256-B spans' powers");
@@ -382,7 +371,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
   const uint8_t *in = a.in;
   uint8_t *out = a.out;
   uint64_t nrec = a.nrec, dbase = 0;
-  if (MODE == kTileDesc || SEG) desc_class_range<MODE>(a, dbase, nrec);
+  if (SEG) seg_range(a, dbase, nrec);
   uint32_t k[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) k[i] = a.key.w[i];
@@ -406,12 +395,9 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     seg_meta_load<MODE, SPAN>(nxt, a.rt, nxt_e, g < nrec, in, out);
   }
 
-  // records per super-tile: 64 (one key lane each), but at most 128 KiB for
-  // descriptor classes of 4 KiB and up (8 tiles), so that a class of tens of
-  // thousands of 16 KiB records still makes thousands of waves
-  constexpr int RPS = (MODE == kTileDesc && L > 2048) ? 64 * 2048 / L : 64;
+  // records per super-tile: 64 (one key lane each)
+  constexpr int RPS = 64;
   constexpr int NTS = RPS / C::RPT;  // tiles per super-tile
-  static_assert(RPS == 64 || (!SEG && NTS >= 1 && RPS % C::RPT == 0), "super-tile shape");
 #pragma unroll 1
   for (uint64_t super0 = (uint64_t)blockIdx.x * RPS; super0 < nrec;
        super0 += (uint64_t)gridDim.x * RPS) {
@@ -420,7 +406,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
   F26 pw[C::LOG2G > 0 && !SEG ? C::LOG2G : 1];  // uniform / keyed: r^BPL, r^(2 BPL), ...
   uint32_t own_q = 0;  // kTileSeg*: the long record of segment super0 + lane
   uint32_t own_k[8], own_nlo = 0, own_nhi = 0;  // keyed modes: this lane's record
-  uint32_t own_in_lo = 0, own_in_hi = 0, own_out_lo = 0, own_out_hi = 0, own_di = 0;
+  uint32_t own_in_lo = 0, own_in_hi = 0, own_out_lo = 0, own_out_hi = 0;
   uint32_t own_cb = 0;  // kTileSeg: first ChaCha block counter - 1 (16 s)
   bool own_bad = false, own_inplace = false;
   uint32_t own_ok = 1u;  // kTileSegXor: the record's tag verified
@@ -460,20 +446,8 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
       uint32_t ki = 0;
       n = 0;
       if (rec < nrec && lane < (uint32_t)RPS) {
-        if (MODE == kTileSessions) {
-          ki = __builtin_nontemporal_load(a.key_idx + rec);
-          n = __builtin_nontemporal_load(a.nonces + rec);
-        } else {
-          own_di = a.idx[dbase + rec];
-          const noise_gpu_record d = a.recs[own_di];
-          ki = d.key_idx;
-          n = d.nonce;
-          own_in_lo = (uint32_t)d.in_off;
-          own_in_hi = (uint32_t)(d.in_off >> 32);
-          own_out_lo = (uint32_t)d.out_off;
-          own_out_hi = (uint32_t)(d.out_off >> 32);
-          own_inplace = in + d.in_off == out + d.out_off;
-        }
+        ki = __builtin_nontemporal_load(a.key_idx + rec);  // kTileSessions
+        n = __builtin_nontemporal_load(a.nonces + rec);
       }
       own_bad = ki >= a.nkeys;
       if (own_bad) ki = 0;
@@ -675,9 +649,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     fail_mask = badk_mask;
     // cross-lane reads stay outside divergent code: a ds_bpermute from a lane
     // that is inactive does not return that lane's value
-    const uint32_t rec_di = MODE == kTileDesc ? (uint32_t)__shfl((int)own_di, src) : 0u;
-    constexpr bool PER_REC_INPL = MODE == kTileDesc || MODE == kTileSegXor;
-    const bool rec_inplace = MODE == kTileDesc ? __shfl((int)own_inplace, src) != 0 : false;
+    constexpr bool PER_REC_INPL = MODE == kTileSegXor;
     uint64_t inpl_seg = 0;  // kTileSegXor: bit r * G = slot r is in place
     if (MODE == kTileSegXor) {
       // a segment of a record whose tag failed: not output as computed.  Slot
@@ -695,16 +667,13 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
                             (want.z ^ tag[2]) | (want.w ^ tag[3]);
       fail_mask |= __ballot(j == 0 && diff != 0u);
       if (j == 0 && valid) {
-        const uint64_t si = MODE == kTileDesc ? (uint64_t)rec_di : rec0 + rho;
-        a.status[si] = bad_key ? 2u : (diff ? 1u : 0u);
+        a.status[rec0 + rho] = bad_key ? 2u : (diff ? 1u : 0u);
       }
     } else if (j == 0) {
       lb[C::REC_SLOTS + rho] = make_uint4(tag[0], tag[1], tag[2], tag[3]);
     }
-    // kTileDesc / kTileSegXor: a failed in-place record is kept, a failed
-    // copy is zeroed
-    const uint64_t inpl_mask = MODE == kTileSegXor ? inpl_seg
-                               : PER_REC_INPL ? __ballot(j == 0 && rec_inplace) : 0ull;
+    // kTileSegXor: a failed in-place record is kept, a failed copy is zeroed
+    const uint64_t inpl_mask = MODE == kTileSegXor ? inpl_seg : 0ull;
     wave_lds_fence();
     if (!DO_XOR) {  // kTileSegPoly: nothing to store; the next tile's DMA
       prev_all = false;
@@ -731,11 +700,10 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     constexpr int NPART = (KEYED && NBUF == 1 && NOUT > 8) ? 2 : 1;
     constexpr int NQ = (NOUT + NPART - 1) / NPART;
     const bool full = nv == (uint32_t)C::RPT;
-    // RECQ (segments, descriptor records of whole KiB): output instruction
-    // q < NDATA holds the 64 data pieces of KiB q % (SPR / 64) of record
-    // q / (SPR / 64) (uniform destination, v_readlane), instruction NDATA
-    // (encrypt) the RPT tags
-    constexpr bool RECQ = SEG || (MODE == kTileDesc && C::SPR % 64 == 0);
+    // RECQ (segments): output instruction q < NDATA holds the 64 data pieces
+    // of KiB q % (SPR / 64) of record q / (SPR / 64) (uniform destination,
+    // v_readlane), instruction NDATA (encrypt) the RPT tags
+    constexpr bool RECQ = SEG;
     auto piece = [&](int q, uint32_t &r, uint32_t &pc, uint32_t &slot, bool &ok) {
       if constexpr (RECW) {
         if (q < NDATA) {
@@ -837,11 +805,6 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
           const uint64_t off = join64((uint32_t)__builtin_amdgcn_readlane((int)own_out_hi, (int)kl),
                                       (uint32_t)__builtin_amdgcn_readlane((int)own_out_lo, (int)kl));
           dst = out + off + 16u * pc;
-        } else if (MODE == kTileDesc) {
-          const uint32_t rs = (uint32_t)t * C::RPT + (r < (uint32_t)C::RPT ? r : 0u);
-          const uint64_t off = ((uint64_t)(uint32_t)__shfl((int)own_out_hi, rs) << 32) |
-                               (uint32_t)__shfl((int)own_out_lo, rs);
-          dst = out + off + 16u * pc;
         } else {
           dst = out + rec0 * a.out_stride +
                 ((CONTIG && !RECW) ? 16ull * g : r * a.out_stride + 16u * pc);
@@ -851,7 +814,7 @@ __global__ __launch_bounds__(64) void k_aead_tile(const TileArgs a) {
     }
     prev_all = ABL == 0 && full && fail_mask == 0;
   }
-  }  // super-tiles (one iteration unless the grid is capped: kTileDesc)
+  }  // super-tiles
 }
 
 }  // namespace noise_amd

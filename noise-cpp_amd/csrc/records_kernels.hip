@@ -10,12 +10,12 @@
 //   2. one launch per class, each reading its slice and count from device
 //      memory:
 //        - tile classes: 16-byte aligned, AD-free records of any length up
-//          to 8 KiB and of exactly 16 KiB, by the smallest capacity (64 ..
-//          16384 B) that holds them -> the LDS-staged masked tile kernel (mtile_kernel.hpp,
+//          to 2 KiB and of exactly 4, 8 and 16 KiB, by the smallest capacity
+//          (64 .. 16384 B) that holds them -> the LDS-staged masked tile kernel (mtile_kernel.hpp,
 //          kMTDesc), one launch per capacity for its exact-size and ragged
 //          records;
-//        - long records: 16-byte aligned, AD-free, 8 KiB < len <= 65535
-//          except exactly 16 KiB (see record_class) -> cut into 1 KiB
+//        - long records: 16-byte aligned, AD-free, 2 KiB < len <= 65535
+//          except exactly 4, 8, 16 KiB (see record_class) -> cut into 1 KiB
 //          segments + a tail (masked 1 KiB tile units).  k_seg_prep
 //          derives each record's one-time key and r powers, ONE tile-kernel
 //          launch (kTileSeg) encrypts every full segment of every long
@@ -134,7 +134,11 @@ __device__ __forceinline__ bool key_row_zero(const uint8_t *keys, uint32_t ki) {
   return (a.x | a.y | a.z | a.w | b.x | b.y | b.z | b.w) == 0u;
 }
 
-// (8 KiB, NOISE_SEG_MID_HI]: segments instead of the 16 KiB masked tile
+// (NOISE_SEG_LO, NOISE_SEG_MID_HI] (not an exact tile size): segments
+// instead of the masked tile of the next capacity
+#ifndef NOISE_SEG_LO
+#define NOISE_SEG_LO 2048
+#endif
 #ifndef NOISE_SEG_MID_HI
 #define NOISE_SEG_MID_HI 16383
 #endif
@@ -169,12 +173,12 @@ __device__ __forceinline__ int record_class(const noise_gpu_record &d, const uin
   // every other length up to 16 KiB: the masked tile class of the smallest
   // capacity that holds it -- the record still sits whole in one wave's
   // tile, so decrypt checks its tag there and reads the ciphertext once
-  // (8 KiB, 16 KiB): the segment path (1 KiB segments + a masked tail unit)
-  // beats the 16 KiB tile, which holds one record per tile and idles up to
-  // half of it: single-length batches of 9000 / 12289 / 16000 / 16383 B run
-  // at 1223 / 1189 / 1219 / 1260 GiB/s against 693 / 904 / 1148 / 1144, and
-  // config 4 is unchanged within its noise (profiles/round6/ab/seg_threshold.md)
-  if (d.len <= 16384u && !(d.len > 8192u && d.len <= (uint32_t)NOISE_SEG_MID_HI)) {
+  // Above 2 KiB (but the exact 4, 8, 16 KiB tiles) the segment path (1 KiB
+  // segments + a masked tail unit) beats the masked tile of the next
+  // capacity: single-length batches of 3000 / 5000 / 9000 / 16000 B at
+  // 1131 / 1205 / 1223 / 1219 GiB/s against 983 / 813 / 693 / 1148, config 4
+  // within its noise (profiles/round6/ab/seg_threshold.md)
+  if (d.len <= 16384u && !(d.len > (uint32_t)NOISE_SEG_LO && d.len <= (uint32_t)NOISE_SEG_MID_HI)) {
     const uint32_t n = d.len;
     const int c = n <= 64u ? 0 : n <= 128u ? 1 : n <= 192u ? 2 : n <= 256u ? 3 : n <= 512u ? 4
                 : n <= 1024u ? 5 : n <= 2048u ? 6 : n <= 4096u ? 7 : n <= 8192u ? 8 : 9;

@@ -127,11 +127,11 @@ int noise_gpu_decrypt_uniform(const uint8_t h_key[32], uint64_t nonce0,
  * Batches of >= 2048 records are load-balanced on the device, stream-ordered
  * (no host synchronisation): records are sorted by class and each class
  * runs its own kernel -- 16-byte aligned AD-free records of any length up to
- * 8192 bytes, and of exactly 16384, on the LDS-staged masked tile kernel,
- * one launch per tile capacity (64, 128, 192, 256, 512 B, 1, 2, 4, 8, 16
- * KiB: the smallest that holds the record; a record sits whole in one wave,
- * and decrypt reads its ciphertext once); aligned AD-free records of
- * 8193..65535 bytes (but 16384) cut into
+ * 2048 bytes, and of exactly 4096, 8192 and 16384, on the LDS-staged
+ * masked tile kernel, one launch per tile capacity (64, 128, 192, 256,
+ * 512 B, 1, 2, 4, 8, 16 KiB: the smallest that holds the record; a record
+ * sits whole in one wave, and decrypt reads its ciphertext once); the other
+ * aligned AD-free records of 2049..65535 bytes cut into
  * 1 KiB segments that ONE tile-kernel launch processes, plus their tails
  * (len % 1024, masked 1 KiB tile units) and a per-record finalize (tag);
  * everything else one lane per record.  Every path checks a record's

@@ -82,6 +82,82 @@ static inline dim3 grid_for(uint64_t n) {
   return dim3((unsigned)((n + kBlock - 1) / kBlock));
 }
 
+// ---- unaligned uniform batches, staged --------------------------------------
+// Records that do not start 16-byte aligned (the Noise wire format packed back
+// to back with a length that is not a multiple of 16: 1000-byte records at
+// strides 1000 / 1016) cannot be LDS-DMA'd piece by piece.  They are copied
+// into an aligned image in the scratch (row stride ceil16(len + 16)), the
+// tile kernels run on it in place, and the outputs are copied back.  The two
+// copies are HBM-bound passes beside a VALU-bound kernel.
+//
+// k_stage_in: thread (record i, piece p) moves source bytes [16p, 16p + 16) of
+// record i (n bytes) to the aligned row: two aligned loads and a byte funnel
+// (a 16-byte aligned block holding a byte of the record never crosses a
+// page); bytes past n are don't-care (the tile kernels mask them).
+__global__ __launch_bounds__(kBlock) void k_stage_in(const uint8_t *in, uint64_t in_stride,
+                                                     uint8_t *s, uint64_t sstride, uint32_t n,
+                                                     uint32_t np, uint64_t nrec) {
+  const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t i = t / np;
+  const uint32_t p = (uint32_t)(t % np);
+  if (i >= nrec) return;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(in + i * in_stride) + 16ull * p;
+  const uint32_t sh = (uint32_t)(a & 15u);
+  const uint4 *b = reinterpret_cast<const uint4 *>(a - sh);
+  const uint32_t have = n - 16u * p < 16u ? n - 16u * p : 16u;  // this piece's record bytes
+  uint4 v = b[0];
+  if (sh) {
+    const uint4 hi = sh + have > 16u ? b[1] : make_uint4(0u, 0u, 0u, 0u);
+    v = extract16(v, hi, sh);
+  }
+  *reinterpret_cast<uint4 *>(s + i * sstride + 16ull * p) = v;
+}
+
+// k_stage_out: thread (record i, block b) writes the 16-byte aligned block b of
+// record i's destination range [D, D + n) (blocks from floor16(D)), only the
+// record's own bytes: whole blocks by one 16-byte store, the partial first and
+// last blocks byte by byte (a neighbouring record may own the rest).  Decrypt:
+// a record whose tag failed is skipped (in place: left as it was) or zeroed.
+__global__ __launch_bounds__(kBlock) void k_stage_out(const uint8_t *s, uint64_t sstride,
+                                                      uint8_t *out, uint64_t out_stride, uint32_t n,
+                                                      uint32_t nb, const uint8_t *status,
+                                                      int keep_failed, uint64_t nrec) {
+  const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t i = t / nb;
+  const uint32_t bi = (uint32_t)(t % nb);
+  if (i >= nrec) return;
+  const uintptr_t d = reinterpret_cast<uintptr_t>(out + i * out_stride);
+  const uintptr_t blk = (d & ~(uintptr_t)15u) + 16ull * bi;
+  const uintptr_t lo = blk > d ? blk : d, hi = blk + 16u < d + n ? blk + 16u : d + n;
+  if (lo >= hi) return;
+  bool zero = false;
+  if (status && status[i] != 0u) {
+    if (keep_failed) return;
+    zero = true;
+  }
+  // byte k of the block = staged byte off + k of the record
+  const int64_t off = (int64_t)blk - (int64_t)d;  // >= -15
+  const int64_t a0 = off >= 0 ? (off & ~(int64_t)15) : -16;
+  const uint32_t sh = (uint32_t)(off - a0);
+  const uint8_t *row = s + i * sstride;
+  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+  const uint4 A = a0 >= 0 ? *reinterpret_cast<const uint4 *>(row + a0) : z;
+  const uint4 B = (sh && a0 + 16 < (int64_t)sstride) ? *reinterpret_cast<const uint4 *>(row + a0 + 16) : z;
+  uint4 v = sh ? extract16(A, B, sh) : A;
+  if (zero) v = z;
+  uint8_t *bp = reinterpret_cast<uint8_t *>(blk);
+  if (lo == blk && hi == blk + 16u) {
+    store16<true>(bp, v, 16);
+  } else {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    for (uint32_t j = (uint32_t)(lo - blk); j < (uint32_t)(hi - blk); ++j)
+      bp[j] = (uint8_t)(w[j >> 2] >> (8u * (j & 3u)));
+  }
+}
+
+// records per call from which staging beats the lane walk
+constexpr uint64_t kStageMin = 1024;
+
 hipError_t launch_aead_uniform(bool decrypt, const uint32_t key[8],
                                uint64_t nonce0, const uint8_t *in,
                                uint64_t in_stride, uint8_t *out,
@@ -199,6 +275,28 @@ hipError_t launch_aead_uniform(bool decrypt, const uint32_t key[8],
     NOISE_MTILE(8192)
     NOISE_MTILE(16384)
 #undef NOISE_MTILE
+  }
+  // unaligned records up to 16 KiB, no AD: staged through an aligned image
+  // (k_stage_in / k_stage_out above), the tile kernels in place on it
+  const bool inplace = in == out && in_stride == out_stride;
+  if (!al && ad_len == 0 && len >= 1 && len <= 16384 && nrec >= kStageMin &&
+      (inplace || in + in_stride * nrec <= out || out + out_stride * nrec <= in)) {
+    const uint64_t sstride = ((uint64_t)len + 31u) & ~15ull;
+    void *mem = nullptr;
+    hipError_t e = records_scratch_get(&mem, nrec * sstride, stream);
+    if (e != hipSuccess) return e;
+    uint8_t *s = static_cast<uint8_t *>(mem);
+    const uint32_t nin = decrypt ? len + 16u : len, nout = decrypt ? len : len + 16u;
+    const uint32_t np = (nin + 15u) / 16u, nb = nout / 16u + 2u;
+    hipLaunchKernelGGL(k_stage_in, grid_for(nrec * np), dim3(kBlock), 0, stream, in, in_stride, s, sstride,
+                       nin, np, nrec);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    e = launch_aead_uniform(decrypt, key, nonce0, s, sstride, s, sstride, len, nullptr, 0, 0, status, nrec,
+                            stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_stage_out, grid_for(nrec * nb), dim3(kBlock), 0, stream, s, sstride, out,
+                       out_stride, nout, nb, decrypt ? status : nullptr, inplace ? 1 : 0, nrec);
+    return hipGetLastError();
   }
   const dim3 g = grid_for(nrec), b(kBlock);
   if (decrypt) {

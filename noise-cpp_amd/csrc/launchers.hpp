@@ -27,6 +27,9 @@ hipError_t launch_aead_records(bool decrypt, const uint8_t *keys,
 
 // zero the records-path scratch of (current device, stream)
 hipError_t records_scratch_wipe(hipStream_t stream);
+// the grow-only scratch of (current device, stream), >= bytes; the records
+// path and the uniform path's staging of unaligned batches share it
+hipError_t records_scratch_get(void **p, size_t bytes, hipStream_t stream);
 // zero + free the scratch and destroy the companion stream cached for
 // (current device, stream); call before destroying `stream`
 hipError_t records_scratch_release(hipStream_t stream);

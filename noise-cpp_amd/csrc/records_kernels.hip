@@ -761,6 +761,10 @@ static hipError_t scratch_get(void **p, size_t bytes, hipStream_t stream) {
   return hipSuccess;
 }
 
+hipError_t records_scratch_get(void **p, size_t bytes, hipStream_t stream) {
+  return scratch_get(p, bytes, stream);
+}
+
 // Zero the scratch of (current device, stream): the long-record table holds
 // key copies, one-time Poly1305 keys and partial sums between the kernels of
 // a call.  Stream-ordered after the call's kernels.

@@ -119,3 +119,69 @@ def test_uniform_ragged(oracle, L, nrec, layout):
     ok = np.ones(nrec, dtype=bool)
     ok[bad] = False
     assert np.array_equal(rows[ok, :L], pt.reshape(nrec, L)[ok])
+
+
+# Unaligned uniform batches of >= 1024 records (aead_kernels.hip stages them
+# through an aligned scratch image for the tile kernels): odd strides and base
+# offsets, the Noise wire format packed back to back, in place; the oracle on
+# every record, gaps untouched, tampered records fail (in place untouched,
+# copies zeroed).  Emulated under ASan by `tools/emu/build/emu_uniform unaligned`.
+UNALIGNED = [1, 17, 100, 1000, 1040, 3000, 5000, 16383]
+
+
+@pytest.mark.parametrize("layout", ["odd", "packed", "in_place"])
+@pytest.mark.parametrize("L", UNALIGNED)
+def test_uniform_unaligned_staged(oracle, L, layout):
+    rng = random.Random(L * 131 + len(layout))
+    nrec = 1100 if L <= 5000 else 1030
+    key, n0 = rng.randbytes(32), rng.getrandbits(40)
+    if layout == "odd":
+        ps, cs, po, co = L + 3, L + 16 + 5, 1, 7
+    elif layout == "packed":
+        ps, cs, po, co = L, L + 16, 3, 3
+    else:
+        ps = cs = L + 16 + 3
+        po = co = 5
+    pt = np.frombuffer(rng.randbytes(nrec * L), dtype=np.uint8)
+    src = np.full(po + ps * nrec + 32, FILL, dtype=np.uint8)
+    src[po:po + ps * nrec].reshape(nrec, ps)[:, :L] = pt.reshape(nrec, L)
+    d_in = torch.from_numpy(src.copy()).cuda()
+    d_ct = d_in if layout == "in_place" else torch.full((co + cs * nrec + 32,), FILL, dtype=torch.uint8,
+                                                         device="cuda")
+    noise_amd.encrypt_uniform(key, n0, d_in, ps, d_ct, cs, L, nrec, in_offset=po, out_offset=co)
+    ct = _np(d_ct).copy()
+    assert oracle.check_uniform(0, key, n0, src[po:], ps, ct[co:], cs, L, nrec) == (0, -1)
+    if cs > L + 16:
+        assert (ct[co:co + cs * nrec].reshape(nrec, cs)[:, L + 16:] == FILL).all()
+    assert (ct[:co] == FILL).all() and (ct[co + cs * nrec:] == FILL).all()
+    bad = {0: 0, nrec // 3: L - 1, nrec - 1: L + 7, nrec // 2: L}
+    for r, off in bad.items():
+        ct[co + r * cs + off] ^= 0x21
+    bad = sorted(bad)
+    d_c2 = torch.from_numpy(ct.copy()).cuda()
+    d_st = torch.full((nrec,), 9, dtype=torch.uint8, device="cuda")
+    if layout == "in_place":
+        d_pt, so, ss = d_c2, co, cs
+    else:
+        d_pt = torch.full((po + ps * nrec + 32,), FILL, dtype=torch.uint8, device="cuda")
+        so, ss = po, ps
+    noise_amd.decrypt_uniform(key, n0, d_c2, cs, d_pt, ss, L, d_st, nrec, in_offset=co, out_offset=so)
+    st, back = _np(d_st), _np(d_pt)
+    want = np.zeros(nrec, dtype=np.uint8)
+    want[bad] = noise_amd.REC_BAD_MAC
+    assert np.array_equal(st, want)
+    rows = back[so:so + ss * nrec].reshape(nrec, ss)
+    ctr = ct[co:co + cs * nrec].reshape(nrec, cs)
+    ok = np.ones(nrec, dtype=bool)
+    ok[bad] = False
+    assert np.array_equal(rows[ok, :L], pt.reshape(nrec, L)[ok])
+    for r in bad:
+        if layout == "in_place":
+            assert rows[r, :L + 16].tobytes() == ctr[r, :L + 16].tobytes()
+        else:
+            assert not rows[r, :L].any()
+    if layout == "in_place":
+        assert np.array_equal(rows[:, L:L + 16], ctr[:, L:L + 16])
+    elif ss > L:
+        assert (rows[:, L:] == FILL).all()
+    assert (back[:so] == FILL).all() and (back[so + ss * nrec:] == FILL).all()

@@ -159,7 +159,108 @@ static void run(uint32_t L, uint64_t seed, bool inplace, uint64_t R) {
   std::free(pt);
 }
 
+// Unaligned records (strides and bases off 16; aead_kernels.hip stages them
+// through an aligned scratch image): the oracle on every record, canary bytes
+// between records untouched, tampered records fail (in place: untouched,
+// copy: zeros).  No store watch: the tile kernels write the scratch image.
+static void run_unaligned(uint32_t L, uint64_t seed, bool inplace, uint64_t R) {
+  const uint64_t sin = inplace ? L + 16 + 3 : L + 3, sct = inplace ? sin : L + 16 + 5;
+  const uint64_t oin = inplace ? 5 : 1, oct = inplace ? 5 : 7;
+  uint8_t key[32];
+  for (int i = 0; i < 32; ++i) key[i] = (uint8_t)(mix64(seed + i) | 1);
+  uint32_t k[8];
+  std::memcpy(k, key, 32);
+  const uint64_t nonce0 = mix64(seed * 3 + L) & 0xffffffffull;
+  std::vector<uint8_t> pt_ref(R * L);
+  for (uint64_t j = 0; j < R * L; ++j) pt_ref[j] = (uint8_t)mix64(seed * 17 + j);
+  const uint64_t nbin = oin + R * sin + 16, nbct = oct + R * sct + 16;
+  uint8_t *bin = (uint8_t *)std::aligned_alloc(16, (nbin + 15) / 16 * 16);
+  uint8_t *bct = inplace ? bin : (uint8_t *)std::aligned_alloc(16, (nbct + 15) / 16 * 16);
+  std::memset(bin, 0xA5, (nbin + 15) / 16 * 16);
+  if (!inplace) std::memset(bct, 0x5A, (nbct + 15) / 16 * 16);
+  uint8_t *pt = bin + oin, *ct = bct + oct;
+  for (uint64_t i = 0; i < R; ++i) std::memcpy(pt + i * sin, pt_ref.data() + i * L, L);
+  hipError_t e = noise_amd::launch_aead_uniform(false, k, nonce0, pt, sin, ct, sct, L, nullptr, 0, 0, nullptr, R, nullptr);
+  CHECK(e == hipSuccess, "unaligned encrypt launch L=%u", L);
+  std::vector<uint8_t> want(L + 16);
+  const uint8_t fill = inplace ? 0xA5 : 0x5A;
+  for (uint64_t i = 0; i < R; ++i) {
+    oracle_noise_encrypt(key, nonce0 + i, nullptr, 0, pt_ref.data() + i * L, L, want.data());
+    CHECK(std::memcmp(ct + i * sct, want.data(), L + 16) == 0, "unaligned encrypt L=%u rec %llu %s", L,
+          (unsigned long long)i, inplace ? "in place" : "copy");
+    for (uint64_t b = L + 16; b < sct; ++b)
+      if (ct[i * sct + b] != fill) {
+        CHECK(false, "unaligned encrypt L=%u rec %llu wrote gap byte %llu", L, (unsigned long long)i,
+              (unsigned long long)b);
+        break;
+      }
+  }
+  if (!inplace) CHECK(bct[0] == fill && bct[oct - 1] == fill, "unaligned encrypt wrote before the first record");
+  std::vector<uint8_t> bad(R, 0);
+  for (uint64_t i = 3; i < R; i += 97) {
+    const uint64_t pos = (i / 97) % 3 == 0 ? L + 15 : (i / 97) % 3 == 1 ? 0 : L - 1;
+    ct[i * sct + pos] ^= 0x40;
+    bad[i] = 1;
+  }
+  std::vector<uint8_t> ct_copy(ct, ct + R * sct);
+  uint8_t *bback = inplace ? bct : (uint8_t *)std::aligned_alloc(16, (nbin + 15) / 16 * 16);
+  if (!inplace) std::memset(bback, 0xC3, (nbin + 15) / 16 * 16);
+  uint8_t *back = inplace ? ct : bback + oin;
+  const uint64_t sb = inplace ? sct : sin;
+  uint8_t *st = (uint8_t *)std::malloc(R);
+  std::memset(st, 9, R);
+  e = noise_amd::launch_aead_uniform(true, k, nonce0, ct, sct, back, sb, L, nullptr, 0, 0, st, R, nullptr);
+  CHECK(e == hipSuccess, "unaligned decrypt launch L=%u", L);
+  for (uint64_t i = 0; i < R; ++i) {
+    if (bad[i]) {
+      CHECK(st[i] == 1, "unaligned status of tampered L=%u rec %llu = %u", L, (unsigned long long)i, st[i]);
+      if (inplace) {
+        CHECK(std::memcmp(back + i * sb, ct_copy.data() + i * sct, L + 16) == 0, "unaligned in-place failure modified L=%u", L);
+      } else {
+        for (uint32_t b = 0; b < L; ++b)
+          if (back[i * sb + b] != 0) {
+            CHECK(false, "unaligned failed copy not zeroed L=%u rec %llu", L, (unsigned long long)i);
+            break;
+          }
+      }
+    } else {
+      CHECK(st[i] == 0, "unaligned status L=%u rec %llu = %u", L, (unsigned long long)i, st[i]);
+      CHECK(std::memcmp(back + i * sb, pt_ref.data() + i * L, L) == 0, "unaligned decrypt L=%u rec %llu %s", L,
+            (unsigned long long)i, inplace ? "in place" : "copy");
+    }
+    if (inplace) {
+      CHECK(std::memcmp(back + i * sb + L, ct_copy.data() + i * sct + L, 16) == 0, "unaligned in-place decrypt wrote the tag L=%u", L);
+    } else {
+      for (uint64_t b = L; b < sb; ++b)
+        if (back[i * sb + b] != 0xC3) {
+          CHECK(false, "unaligned decrypt L=%u rec %llu wrote gap byte %llu", L, (unsigned long long)i, (unsigned long long)b);
+          break;
+        }
+    }
+  }
+  std::free(st);
+  if (!inplace) {
+    std::free(bct);
+    std::free(bback);
+  }
+  std::free(bin);
+}
+
 int main(int argc, char **argv) {
+  if (argc > 1 && std::strcmp(argv[1], "unaligned") == 0) {
+    // records >= kStageMin (1024) take the staged path
+    const uint32_t lens[] = {1, 17, 100, 1000, 1023, 1040, 3000, 5000};
+    for (uint32_t L : lens) {
+      const uint64_t R = L > 2048 ? 1030 : 1100;
+      run_unaligned(L, 11 + L, false, R);
+      run_unaligned(L, 13 + L, true, R);
+      std::printf("unaligned L=%u R=%llu ok so far (%d failures)\n", L, (unsigned long long)R, fails);
+      std::fflush(stdout);
+    }
+    noise_amd::records_scratch_release(nullptr);  // the staging scratch
+    std::printf("%s (%d failures)\n", fails ? "FAIL" : "ok", fails);
+    return fails ? 1 : 0;
+  }
   const uint64_t seed = argc > 1 ? std::strtoull(argv[1], nullptr, 0) : 3;
   std::vector<uint32_t> lens;
   for (int i = 2; i < argc; ++i) lens.push_back((uint32_t)std::strtoul(argv[i], nullptr, 0));

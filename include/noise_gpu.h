@@ -94,9 +94,13 @@ int noise_gpu_device_count(int *count);
  * (the hot path); any other len of 1..16384 with 16-byte aligned pointers
  * and strides and no AD on the masked tile kernel, at the smallest tile
  * capacity >= len (the powers of two above and 320, 384, 448, 768, 1280,
- * 1536, 1792, 2304, 2560, 3072, 5120); other shapes (AD, unaligned records,
- * len > 16384) one record per lane (vector path when 16-byte aligned with
- * len % 16 == 0, byte-granular otherwise).
+ * 1536, 1792, 2304, 2560, 3072, 5120); unaligned records (strides or bases
+ * not multiples of 16) of len <= 16384 without AD, in batches of >= 1024
+ * records that do not partially overlap, are copied into an aligned image in
+ * the library's scratch for (device, stream) (noise_gpu_scratch_wipe clears
+ * it), processed there and copied back; other shapes (AD, len > 16384, small
+ * unaligned batches) one record per lane (vector path when 16-byte aligned
+ * with len % 16 == 0, byte-granular otherwise).
  * Key handling: h_key is copied into the kernel's argument block (kernarg
  * memory) by value, so the 32-byte key stays in that launch's kernarg
  * segment after the call, like any kernel argument; the runtime reuses,

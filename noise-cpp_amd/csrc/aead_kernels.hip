@@ -155,8 +155,12 @@ __global__ __launch_bounds__(kBlock) void k_stage_out(const uint8_t *s, uint64_t
   }
 }
 
-// records per call from which staging beats the lane walk
+// records per call from which staging beats the lane walk; scratch per slice
 constexpr uint64_t kStageMin = 1024;
+#ifndef NOISE_STAGE_BYTES
+#define NOISE_STAGE_BYTES (1ull << 30)
+#endif
+constexpr uint64_t kStageBytes = NOISE_STAGE_BYTES;
 
 hipError_t launch_aead_uniform(bool decrypt, const uint32_t key[8],
                                uint64_t nonce0, const uint8_t *in,
@@ -281,22 +285,30 @@ hipError_t launch_aead_uniform(bool decrypt, const uint32_t key[8],
   const bool inplace = in == out && in_stride == out_stride;
   if (!al && ad_len == 0 && len >= 1 && len <= 16384 && nrec >= kStageMin &&
       (inplace || in + in_stride * nrec <= out || out + out_stride * nrec <= in)) {
+    // in slices of at most kStageBytes of scratch (stream-ordered reuse)
     const uint64_t sstride = ((uint64_t)len + 31u) & ~15ull;
+    const uint64_t per = kStageBytes / sstride > kStageMin ? kStageBytes / sstride : kStageMin;
+    const uint64_t cap = nrec < per ? nrec : per;
     void *mem = nullptr;
-    hipError_t e = records_scratch_get(&mem, nrec * sstride, stream);
+    hipError_t e = records_scratch_get(&mem, cap * sstride, stream);
     if (e != hipSuccess) return e;
     uint8_t *s = static_cast<uint8_t *>(mem);
     const uint32_t nin = decrypt ? len + 16u : len, nout = decrypt ? len : len + 16u;
     const uint32_t np = (nin + 15u) / 16u, nb = nout / 16u + 2u;
-    hipLaunchKernelGGL(k_stage_in, grid_for(nrec * np), dim3(kBlock), 0, stream, in, in_stride, s, sstride,
-                       nin, np, nrec);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    e = launch_aead_uniform(decrypt, key, nonce0, s, sstride, s, sstride, len, nullptr, 0, 0, status, nrec,
-                            stream);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_stage_out, grid_for(nrec * nb), dim3(kBlock), 0, stream, s, sstride, out,
-                       out_stride, nout, nb, decrypt ? status : nullptr, inplace ? 1 : 0, nrec);
-    return hipGetLastError();
+    for (uint64_t r0 = 0; r0 < nrec; r0 += cap) {
+      const uint64_t n = nrec - r0 < cap ? nrec - r0 : cap;
+      hipLaunchKernelGGL(k_stage_in, grid_for(n * np), dim3(kBlock), 0, stream, in + r0 * in_stride, in_stride,
+                         s, sstride, nin, np, n);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+      e = launch_aead_uniform(decrypt, key, nonce0 + r0, s, sstride, s, sstride, len, nullptr, 0, 0,
+                              status ? status + r0 : nullptr, n, stream);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(k_stage_out, grid_for(n * nb), dim3(kBlock), 0, stream, s, sstride,
+                         out + r0 * out_stride, out_stride, nout, nb, decrypt ? status + r0 : nullptr,
+                         inplace ? 1 : 0, n);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipSuccess;
   }
   const dim3 g = grid_for(nrec), b(kBlock);
   if (decrypt) {

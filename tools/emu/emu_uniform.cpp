@@ -249,7 +249,11 @@ static void run_unaligned(uint32_t L, uint64_t seed, bool inplace, uint64_t R) {
 int main(int argc, char **argv) {
   if (argc > 1 && std::strcmp(argv[1], "unaligned") == 0) {
     // records >= kStageMin (1024) take the staged path
-    const uint32_t lens[] = {1, 17, 100, 1000, 1023, 1040, 3000, 5000};
+    std::vector<uint32_t> lens = {1, 17, 100, 1000, 1023, 1040, 3000, 5000};
+    if (argc > 2) {
+      lens.clear();
+      for (int i = 2; i < argc; ++i) lens.push_back((uint32_t)std::strtoul(argv[i], nullptr, 0));
+    }
     for (uint32_t L : lens) {
       const uint64_t R = L > 2048 ? 1030 : 1100;
       run_unaligned(L, 11 + L, false, R);
